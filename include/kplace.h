@@ -1,0 +1,206 @@
+/*
+ * kplace.h — C-ABI of the MI355X-native batch placement engine (libkplace.so).
+ *
+ * This is the drop-in boundary for kubeinfer's placement hot path. The
+ * reference (Moore-Z/Kubernetes-Native-Distributed-AI-Job-Scheduler, Go module
+ * github.com/Moore-Z/kubeinfer) has no FFI and no placement code of its own:
+ *   - its per-job driver is LLMServiceReconciler.Reconcile
+ *     (internal/controller/llmservice_controller.go:66-174), one CR at a time;
+ *   - it builds one Deployment per CR with Spec.Replicas identical pods
+ *     (desiredDeployment, llmservice_controller.go:182-313) and leaves the node
+ *     choice of each pod to the external kube-scheduler (Filter/Score/selectHost).
+ * Every entry point below replaces that per-pod Filter/Score/Bind pass with one
+ * batched solve of the whole pending queue; the Go caller a maintainer would add
+ * (pkg/placement, cgo) is shown in INTEGRATION.md. The placement semantics are
+ * frozen in DESIGN.md §2 ("Placement spec"), restated on the CPU in oracle/.
+ *
+ * Conventions (all entry points):
+ *   - SoA, row-major by dimension: req[d*J + j], cap[d*N + n], used[d*N + n].
+ *   - Caller owns every buffer; the library copies what it needs and retains
+ *     no caller pointer after return.
+ *   - Errors are negative int codes (KP_E*), never aborts or C++ exceptions.
+ *   - One call at a time per kp_ctx (internal mutex). Every entry calls
+ *     hipSetDevice itself, so calls may come from any OS thread (cgo hops
+ *     threads between calls).
+ */
+#ifndef KPLACE_H
+#define KPLACE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KP_ABI_VERSION 1
+
+/* ---- limits ------------------------------------------------------------ */
+#define KP_MAX_DIMS 8       /* resource dimensions per job/node               */
+#define KP_MAX_CAND 32       /* top-K candidate nodes kept per unit per round  */
+#define KP_MAX_GANG 64      /* members of one all-or-nothing gang             */
+#define KP_MAX_VALUE ((int64_t)1 << 56) /* bound on req/cap/used entries       */
+
+/* ---- error codes -------------------------------------------------------- */
+#define KP_OK 0
+#define KP_EINVAL (-1)   /* malformed snapshot / params / arguments            */
+#define KP_EHIP (-2)     /* HIP runtime error                                  */
+#define KP_ERCCL (-3)    /* RCCL error (multi-GPU contexts)                    */
+#define KP_ENOMEM (-4)   /* host or device allocation failed                   */
+#define KP_ESTATE (-5)   /* call order violated (e.g. solve before load)       */
+#define KP_ENODEV (-6)   /* no usable gfx950 device                            */
+
+/* ---- score modes -------------------------------------------------------- */
+#define KP_SCORE_MOST_ALLOCATED 0  /* bin-pack (kube-scheduler MostAllocated)  */
+#define KP_SCORE_LEAST_ALLOCATED 1 /* spread  (kube-scheduler LeastAllocated) */
+
+/* ---- node tie-break modes ------------------------------------------------ */
+#define KP_TIE_NODE_INDEX 0 /* equal scores: lowest node index wins           */
+#define KP_TIE_ROTATED 1    /* equal scores: per-job Weyl rotation of the node
+                               index (deterministic stand-in for
+                               kube-scheduler's random selectHost)            */
+
+/* ---- score sentinels ---------------------------------------------------- */
+#define KP_SCORE_INFEASIBLE (-1) /* score-matrix entry of an infeasible pair  */
+#define KP_SCORE_NONE (-1)       /* score_of_job of an unplaced job           */
+
+/* ---- status of a job after a solve -------------------------------------- */
+#define KP_JOB_PLACED 0
+#define KP_JOB_NO_FIT 1      /* no node can host it (or its gang) any more    */
+#define KP_JOB_ROUND_LIMIT 2 /* still unresolved when max_rounds ran out      */
+
+/*
+ * Snapshot of the pending queue and the node table.
+ * Job side, from the LLMService CRD (api/v1/llmservice_types.go:25-52): one
+ * job = one replica; the Spec.Replicas replicas of one CR form one gang
+ * (contiguous job indices, identical req/prio, all-or-nothing).
+ */
+typedef struct kp_snapshot {
+  int32_t J, N, D;
+  const int64_t *req;          /* [D*J] >= 0                                  */
+  const int64_t *cap;          /* [D*N] >= 0                                  */
+  const int64_t *used;         /* [D*N] 0 <= used <= cap; NULL = all zero     */
+  const int32_t *prio;         /* [J] higher first; NULL = all 0              */
+  const int32_t *gang_id;      /* [J] <0 = singleton; NULL = all singletons   */
+  const int32_t *gang_size;    /* [J] checked against the run length; NULL ok */
+  const int32_t *topo_domain;  /* [N] >= 0 (rack / xGMI island); NULL = n     */
+} kp_snapshot;
+
+/* Scoring / assignment knobs (manager flags in the Go host). */
+typedef struct kp_params {
+  int32_t w_dim[KP_MAX_DIMS]; /* per-dim utilisation weight, 0..65535         */
+  int32_t score_mode;         /* KP_SCORE_*                                   */
+  int32_t gpu_dim;            /* dim holding the GPU count, -1 = none         */
+  int32_t w_gpu_fit;          /* bonus when a job takes exactly the node's
+                                 remaining free GPUs, 0..2^20                 */
+  int32_t w_spread;           /* penalty per same-gang member already planned
+                                 into the node's topo domain, 0..2^20         */
+  int32_t tie_mode;           /* KP_TIE_*                                     */
+  uint32_t tie_seed;          /* salt of the rotated tie-break                */
+  int32_t max_rounds;         /* 0 = until every unit is resolved             */
+  int32_t n_cand;             /* top-K candidates per unit, 1..KP_MAX_CAND    */
+  int32_t util_scale;         /* per-dim utilisation scale S, 1..1024
+                                 (100 = kube-scheduler MaxNodeScore)          */
+  int32_t max_passes;         /* acceptance passes per round, 1..64           */
+} kp_params;
+
+/* Fills *p with the documented defaults. */
+void kp_params_default(kp_params *p);
+
+typedef struct kp_result {
+  int32_t *node_of_job;  /* [J] node index, -1 = unplaced                     */
+  int32_t *score_of_job; /* [J] snapshot score of the chosen node, -1 = none  */
+  int32_t *status_of_job;/* [J] KP_JOB_*; NULL = not wanted                   */
+  int64_t *used_out;     /* [D*N] node usage after commit; NULL = not wanted  */
+  /* filled by the library: */
+  int32_t rounds;        /* auction rounds executed                           */
+  int32_t passes;        /* acceptance passes executed (all rounds)           */
+  int32_t placed_jobs;
+  int32_t unplaced_jobs;
+  int32_t units;         /* gangs + singletons                                */
+  int64_t pairs_scored;  /* sum over rounds of (active units x N)             */
+} kp_result;
+
+/* ---- context ------------------------------------------------------------- */
+typedef struct kp_ctx kp_ctx;
+
+typedef struct kp_config {
+  int32_t device;        /* HIP device ordinal (-1 = current)                 */
+  int32_t world_size;    /* 1 = single GPU; >1 = one process per GPU          */
+  int32_t rank;          /* this process' rank in [0, world_size)             */
+  const void *nccl_id;   /* 128-byte ncclUniqueId from kp_dist_unique_id on
+                            rank 0, broadcast by the caller; NULL if world 1  */
+  int64_t max_pairs_matrix; /* cap on score-matrix entries per chunk
+                               (0 = library default)                         */
+} kp_config;
+
+int kp_create(kp_ctx **out, const kp_config *cfg);
+void kp_destroy(kp_ctx *ctx);
+const char *kp_strerror(int code);
+int kp_abi_version(void);
+/* Writes the 128-byte RCCL unique id for a multi-process context. */
+int kp_dist_unique_id(void *out128);
+
+/*
+ * One-shot placement: validate + upload the snapshot, solve, download.
+ * Synchronous. Replaces one kube-scheduler cycle per pending pod.
+ */
+int kp_place(kp_ctx *ctx, const kp_snapshot *s, const kp_params *p,
+             kp_result *r);
+
+/* ---- staged interface (device-resident snapshot, streaming churn) -------- */
+/* Upload the node table; it stays resident and is updated by every solve. */
+int kp_load_nodes(kp_ctx *ctx, int32_t N, int32_t D, const int64_t *cap,
+                  const int64_t *used, const int32_t *topo_domain);
+/* Upload (validate, group into gangs, rank) the pending queue. */
+int kp_load_jobs(kp_ctx *ctx, int32_t J, const int64_t *req,
+                 const int32_t *prio, const int32_t *gang_id,
+                 const int32_t *gang_size);
+/* Solve the loaded queue against the resident node table and commit the
+   accepted placements into it. Inputs must already be resident. */
+int kp_solve(kp_ctx *ctx, const kp_params *p, kp_result *stats);
+/* Copy the last solve's per-job outputs (and optionally node usage) out. */
+int kp_fetch(kp_ctx *ctx, kp_result *r);
+/* Streaming churn: used[d][node_idx[k]] += delta[d*K + k] (negative = job
+   completion). Fails with KP_EINVAL if a node would leave [0, cap]. */
+int kp_apply_delta(kp_ctx *ctx, const int32_t *node_idx, const int64_t *delta,
+                   int32_t K);
+/* Restore the resident node usage to what the last kp_load_nodes uploaded
+   (device-side copy; for repeated what-if solves on one snapshot). */
+int kp_reset_nodes(kp_ctx *ctx);
+
+/*
+ * Filter + score pass only (the materialised outputs the north_star names):
+ * for jobs [job_lo, job_hi) of the loaded queue against the resident node
+ * table, writes score[(j-job_lo)*N + n] (KP_SCORE_INFEASIBLE if the job does
+ * not fit) and the feasibility bitmask mask[(j-job_lo)*ceil(N/64) + n/64]
+ * bit n%64. Either output may be NULL.
+ */
+int kp_score(kp_ctx *ctx, const kp_params *p, int32_t job_lo, int32_t job_hi,
+             int32_t *score, uint64_t *mask);
+
+/* Timing of the last kp_solve, measured with HIP events on the solve stream. */
+typedef struct kp_timing {
+  double solve_ms;          /* whole device solve (first launch .. last)     */
+  double score_ms;          /* sum of filter+score kernel time               */
+  double select_ms;         /* sum of top-K select kernel time               */
+  double accept_ms;         /* plan + exchange + acceptance + commit         */
+  int64_t score_launches;
+  int64_t score_bytes;      /* algorithmic bytes of the filter+score kernels */
+  int64_t select_bytes;     /* algorithmic bytes of the select kernels       */
+} kp_timing;
+int kp_last_timing(kp_ctx *ctx, kp_timing *t);
+
+/* Enable/disable per-kernel HIP-event timing (off by default: it adds
+   event records between launches). */
+int kp_set_profiling(kp_ctx *ctx, int enable);
+
+/* Host-side helper for the snapshot packer: parses an LLMService GPUMemory
+   string (CRD pattern ^\d+(Gi|Mi)$, ai.ruijie.io_llmservices.yaml:48-51) into
+   MiB. "" -> 0. Returns KP_EINVAL on pattern mismatch or int64 overflow. */
+int kp_parse_gpu_memory(const char *s, int64_t *mib);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KPLACE_H */

@@ -1,0 +1,786 @@
+// kp_api.cpp — C-ABI entry points and host orchestration of libkplace.
+//
+// The boundary replaces kubeinfer's one-CR-at-a-time driver
+// (LLMServiceReconciler.Reconcile, internal/controller/llmservice_controller.go:66-174)
+// and the external kube-scheduler's per-pod Filter/Score/selectHost/Bind with
+// one batched solve. Host code here validates, groups the queue
+// into gangs (one LLMService CR = Spec.Replicas identical replicas,
+// llmservice_controller.go:182-203), ranks units, and drives the round/pass
+// loop; every data-parallel step runs in kp_kernels.hip on the GPU. There is
+// no CPU fallback: without a gfx950 device kp_create fails with KP_ENODEV.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <new>
+
+#include "kp_internal.hpp"
+
+namespace {
+thread_local std::string g_err;
+}
+
+void kp_set_error(const char *what, hipError_t e) {
+  g_err = std::string(what) + ": " + hipGetErrorString(e);
+}
+
+namespace kp {
+int launch_pack_exchange(kp_ctx *c, int32_t A, int32_t K);
+
+static uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+
+// ---- validation, identical to oracle/kp_oracle.c check_params/check_nodes ----
+static int check_params(const kp_params *p, int32_t D) {
+  if (!p) return KP_EINVAL;
+  for (int d = 0; d < KP_MAX_DIMS; ++d)
+    if (p->w_dim[d] < 0 || p->w_dim[d] > 65535) return KP_EINVAL;
+  if (p->score_mode != KP_SCORE_MOST_ALLOCATED && p->score_mode != KP_SCORE_LEAST_ALLOCATED)
+    return KP_EINVAL;
+  if (p->gpu_dim < -1 || p->gpu_dim >= D) return KP_EINVAL;
+  if (p->w_gpu_fit < 0 || p->w_gpu_fit > (1 << 20)) return KP_EINVAL;
+  if (p->w_spread < 0 || p->w_spread > (1 << 20)) return KP_EINVAL;
+  if (p->tie_mode != KP_TIE_NODE_INDEX && p->tie_mode != KP_TIE_ROTATED) return KP_EINVAL;
+  if (p->max_rounds < 0) return KP_EINVAL;
+  if (p->n_cand < 1 || p->n_cand > KP_MAX_CAND) return KP_EINVAL;
+  if (p->util_scale < 1 || p->util_scale > 1024) return KP_EINVAL;
+  if (p->max_passes < 1 || p->max_passes > 64) return KP_EINVAL;
+  return KP_OK;
+}
+
+template <typename T>
+static int dalloc(T **p, size_t n) {
+  if (*p) {
+    (void)hipFree(*p);
+    *p = nullptr;
+  }
+  if (n == 0) n = 1;
+  if (hipMalloc(reinterpret_cast<void **>(p), n * sizeof(T)) != hipSuccess) {
+    *p = nullptr;
+    return KP_ENOMEM;
+  }
+  return KP_OK;
+}
+
+#define KP_TRY(expr)          \
+  do {                        \
+    int rc_ = (expr);         \
+    if (rc_ != KP_OK) return rc_; \
+  } while (0)
+
+static int ensure_nodes(kp_ctx *c, int32_t N, int32_t D) {
+  if (N <= c->cap_N && D == c->D && c->d.cap) return KP_OK;
+  const int32_t n = std::max(N, 64);
+  KP_TRY(dalloc(&c->d.cap, (size_t)D * n));
+  KP_TRY(dalloc(&c->d.used, (size_t)D * n));
+  KP_TRY(dalloc(&c->d.used0, (size_t)D * n));
+  KP_TRY(dalloc(&c->d.R, (size_t)D * n));
+  KP_TRY(dalloc(&c->d.base, (size_t)n));
+  KP_TRY(dalloc(&c->d.topo, (size_t)n));
+  KP_TRY(dalloc(&c->d.heads, 2 * (size_t)n));
+  c->cap_N = n;
+  return KP_OK;
+}
+
+static int ensure_units(kp_ctx *c, int32_t U, int32_t J) {
+  const int32_t K = KP_MAX_CAND;
+  if (U > c->cap_U) {
+    const size_t u = (size_t)std::max(U, 64);
+    KP_TRY(dalloc(&c->d.leader, u));
+    KP_TRY(dalloc(&c->d.size, u));
+    KP_TRY(dalloc(&c->d.status, u));
+    KP_TRY(dalloc(&c->d.salt, u));
+    KP_TRY(dalloc(&c->d.act_local, u));
+    KP_TRY(dalloc(&c->d.cand_local, u * K));
+    KP_TRY(dalloc(&c->d.open, u));
+    KP_TRY(dalloc(&c->d.unit_bad, u));
+    KP_TRY(dalloc(&c->d.st_node, u * K));
+    KP_TRY(dalloc(&c->d.st_count, u * K));
+    KP_TRY(dalloc(&c->d.st_off, u * K));
+    KP_TRY(dalloc(&c->d.st_score, u * K));
+    KP_TRY(dalloc(&c->d.st_n, u + 1));
+    KP_TRY(dalloc(&c->d.st_pos, u + 1));
+    const size_t pm = u * K;  // max proposals per pass
+    KP_TRY(dalloc(&c->d.p_slot, pm));
+    KP_TRY(dalloc(&c->d.p_node, pm));
+    KP_TRY(dalloc(&c->d.p_count, pm));
+    KP_TRY(dalloc(&c->d.p_off, pm));
+    KP_TRY(dalloc(&c->d.p_score, pm));
+    KP_TRY(dalloc(&c->d.k_in, pm));
+    KP_TRY(dalloc(&c->d.k_out, pm));
+    KP_TRY(dalloc(&c->d.v_in, pm));
+    KP_TRY(dalloc(&c->d.v_out, pm));
+    KP_TRY(dalloc(&c->d.p_ok, pm));
+    KP_TRY(dalloc(&c->d.counters, 64));
+    c->d.temp_bytes = rocprim_temp_bytes((int32_t)std::min<size_t>(pm, INT32_MAX));
+    KP_TRY(dalloc(reinterpret_cast<uint8_t **>(&c->d.temp), c->d.temp_bytes));
+    if (c->world > 1) {
+      KP_TRY(dalloc(&c->d.act, u));
+      KP_TRY(dalloc(&c->d.cand, u * K));
+      KP_TRY(dalloc(&c->d.xg_counts, (size_t)c->world));
+      KP_TRY(dalloc(&c->d.xg_send, u * (K + 1)));
+      KP_TRY(dalloc(&c->d.xg_recv, (size_t)c->world * u * (K + 1)));
+    } else {
+      c->d.act = c->d.act_local;
+      c->d.cand = c->d.cand_local;
+    }
+    c->cap_U = (int32_t)u;
+  }
+  if (J > c->cap_J) {
+    const size_t j = (size_t)std::max(J, 64);
+    KP_TRY(dalloc(&c->d.job_node, j));
+    KP_TRY(dalloc(&c->d.job_score, j));
+    KP_TRY(dalloc(&c->d.job_status, j));
+    c->cap_J = (int32_t)j;
+  }
+  return KP_OK;
+}
+
+static int ensure_q(kp_ctx *c, int32_t U, int32_t D) {
+  static thread_local int32_t dummy;
+  (void)dummy;
+  return dalloc(&c->d.q, (size_t)D * std::max(U, 1));
+}
+
+static int ensure_matrix(kp_ctx *c, int32_t rows) {
+  const int32_t Ns = (c->N + 63) & ~63;
+  if (rows <= c->cap_rows && c->d.score) return KP_OK;
+  KP_TRY(dalloc(&c->d.score, (size_t)rows * Ns));
+  KP_TRY(dalloc(&c->d.mask, (size_t)rows * (Ns / 64)));
+  c->cap_rows = rows;
+  return KP_OK;
+}
+
+static ScoreParams make_sp(const kp_ctx *c, const kp_params *p) {
+  ScoreParams sp{};
+  sp.D = c->D;
+  sp.N = c->N;
+  for (int d = 0; d < KP_MAX_DIMS; ++d) sp.w[d] = p->w_dim[d];
+  sp.most_allocated = p->score_mode == KP_SCORE_MOST_ALLOCATED;
+  sp.gpu_dim = p->gpu_dim;
+  sp.w_gpu_fit = p->w_gpu_fit;
+  sp.w_spread = p->w_spread;
+  sp.tie_rotated = p->tie_mode == KP_TIE_ROTATED;
+  sp.n_cand = p->n_cand;
+  return sp;
+}
+
+// R table and LeastAllocated base depend on (S, mode, weights): rebuild on change
+static int prep_for(kp_ctx *c, const kp_params *p) {
+  bool same = c->util_scale_loaded == p->util_scale && c->mode_loaded == p->score_mode;
+  for (int d = 0; d < KP_MAX_DIMS; ++d) same = same && c->w_loaded[d] == p->w_dim[d];
+  if (same) return KP_OK;
+  KP_TRY(launch_prep_nodes(c, p->util_scale, p->score_mode == KP_SCORE_MOST_ALLOCATED,
+                           p->w_dim));
+  c->util_scale_loaded = p->util_scale;
+  c->mode_loaded = p->score_mode;
+  for (int d = 0; d < KP_MAX_DIMS; ++d) c->w_loaded[d] = p->w_dim[d];
+  return KP_OK;
+}
+
+static int64_t rows_per_chunk(const kp_ctx *c) {
+  const int64_t Ns = (c->N + 63) & ~63;
+  int64_t maxp = c->max_pairs_matrix > 0 ? c->max_pairs_matrix : (int64_t)1 << 30;
+  int64_t r = std::max<int64_t>(1, maxp / std::max<int64_t>(Ns, 64));
+  return std::min<int64_t>(r, INT32_MAX / std::max<int64_t>(Ns, 64));
+}
+
+struct EvPair {
+  hipEvent_t a = nullptr, b = nullptr;
+};
+
+}  // namespace kp
+
+using namespace kp;
+
+extern "C" {
+
+void kp_params_default(kp_params *p) {
+  if (!p) return;
+  static const int32_t w[KP_MAX_DIMS] = {1, 1, 4, 2, 1, 1, 1, 1};
+  std::memset(p, 0, sizeof *p);
+  for (int d = 0; d < KP_MAX_DIMS; ++d) p->w_dim[d] = w[d];
+  p->score_mode = KP_SCORE_MOST_ALLOCATED;
+  p->gpu_dim = 2;
+  p->w_gpu_fit = 1024;
+  p->w_spread = 256;
+  p->tie_mode = KP_TIE_ROTATED;
+  p->tie_seed = 0x6B706C61u;
+  p->max_rounds = 0;
+  p->n_cand = 16;
+  p->util_scale = 100;
+  p->max_passes = 16;
+}
+
+int kp_abi_version(void) { return KP_ABI_VERSION; }
+
+const char *kp_strerror(int code) {
+  switch (code) {
+    case KP_OK: return "ok";
+    case KP_EINVAL: return "invalid argument";
+    case KP_EHIP: return g_err.empty() ? "HIP runtime error" : g_err.c_str();
+    case KP_ERCCL: return g_err.empty() ? "RCCL error" : g_err.c_str();
+    case KP_ENOMEM: return "out of memory";
+    case KP_ESTATE: return "call order violated";
+    case KP_ENODEV: return "no usable gfx950 device";
+  }
+  return "unknown error";
+}
+
+int kp_dist_unique_id(void *out128) {
+  if (!out128) return KP_EINVAL;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return KP_ERCCL;
+  static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
+  std::memcpy(out128, &id, sizeof id);
+  return KP_OK;
+}
+
+int kp_create(kp_ctx **out, const kp_config *cfg) {
+  if (!out) return KP_EINVAL;
+  *out = nullptr;
+  kp_config def{};
+  def.device = -1;
+  def.world_size = 1;
+  if (!cfg) cfg = &def;
+  if (cfg->world_size < 1 || cfg->rank < 0 || cfg->rank >= cfg->world_size) return KP_EINVAL;
+  if (cfg->world_size > 1 && !cfg->nccl_id) return KP_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return KP_ENODEV;
+  int dev = cfg->device;
+  if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return KP_ENODEV;
+  if (dev >= ndev) return KP_ENODEV;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return KP_ENODEV;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return KP_ENODEV;
+  kp_ctx *c = new (std::nothrow) kp_ctx();
+  if (!c) return KP_ENOMEM;
+  c->device = dev;
+  c->world = cfg->world_size;
+  c->rank = cfg->rank;
+  c->max_pairs_matrix = cfg->max_pairs_matrix;
+  if (hipSetDevice(dev) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void **>(&c->pinned), 4096, hipHostMallocDefault) !=
+          hipSuccess) {
+    delete c;
+    return KP_EHIP;
+  }
+  if (c->world > 1) {
+    ncclUniqueId id;
+    std::memcpy(&id, cfg->nccl_id, sizeof id);
+    ncclComm_t comm;
+    if (ncclCommInitRank(&comm, c->world, id, c->rank) != ncclSuccess) {
+      kp_destroy(c);
+      return KP_ERCCL;
+    }
+    c->nccl_comm = comm;
+  }
+  *out = c;
+  return KP_OK;
+}
+
+void kp_destroy(kp_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->nccl_comm) ncclCommDestroy(static_cast<ncclComm_t>(c->nccl_comm));
+  DevState &d = c->d;
+  void *ptrs[] = {d.cap, d.used, d.used0, d.R, d.base, d.topo, d.q, d.leader, d.size, d.status, d.salt,
+                  d.job_node, d.job_score, d.job_status, d.act_local, d.cand_local, d.score,
+                  d.mask, d.open, d.unit_bad, d.st_node, d.st_count, d.st_off, d.st_score,
+                  d.st_n, d.st_pos, d.p_slot, d.p_node, d.p_count, d.p_off, d.p_score, d.k_in,
+                  d.k_out, d.v_in, d.v_out, d.p_ok, d.heads, d.counters, d.temp, d.xg_counts,
+                  d.xg_send, d.xg_recv};
+  for (void *p : ptrs)
+    if (p) (void)hipFree(p);
+  if (c->world > 1) {
+    if (d.act) (void)hipFree(d.act);
+    if (d.cand) (void)hipFree(d.cand);
+  }
+  if (c->pinned) (void)hipHostFree(c->pinned);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int kp_set_profiling(kp_ctx *c, int enable) {
+  if (!c) return KP_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->profiling = enable != 0;
+  return KP_OK;
+}
+
+int kp_last_timing(kp_ctx *c, kp_timing *t) {
+  if (!c || !t) return KP_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  *t = c->timing;
+  return KP_OK;
+}
+
+// ---------------------------------------------------------------------------
+int kp_load_nodes(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap, const int64_t *used,
+                  const int32_t *topo) {
+  if (!c) return KP_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (N < 0 || D < 1 || D > KP_MAX_DIMS || (N > 0 && !cap)) return KP_EINVAL;
+  for (int64_t i = 0; i < (int64_t)D * N; ++i) {
+    const int64_t cc = cap[i], u = used ? used[i] : 0;
+    if (cc < 0 || cc > KP_MAX_VALUE || u < 0 || u > cc) return KP_EINVAL;
+  }
+  if (topo)
+    for (int32_t n = 0; n < N; ++n)
+      if (topo[n] < 0) return KP_EINVAL;
+  KP_HIP(hipSetDevice(c->device));
+  try {
+    c->h_cap.assign(cap, cap + (size_t)D * N);
+    c->h_used.assign((size_t)D * N, 0);
+    if (used) std::copy(used, used + (size_t)D * N, c->h_used.begin());
+    c->h_topo.resize(N);
+    for (int32_t n = 0; n < N; ++n) c->h_topo[n] = topo ? topo[n] : n;
+  } catch (const std::bad_alloc &) {
+    return KP_ENOMEM;
+  }
+  if (D != c->D) c->jobs_loaded = false;  // request layout depends on D
+  KP_TRY(ensure_nodes(c, N, D));
+  c->N = N;
+  c->D = D;
+  if (N > 0) {
+    KP_HIP(hipMemcpyAsync(c->d.cap, c->h_cap.data(), sizeof(int64_t) * D * N,
+                          hipMemcpyHostToDevice, c->stream));
+    KP_HIP(hipMemcpyAsync(c->d.used, c->h_used.data(), sizeof(int64_t) * D * N,
+                          hipMemcpyHostToDevice, c->stream));
+    KP_HIP(hipMemcpyAsync(c->d.used0, c->d.used, sizeof(int64_t) * D * N,
+                          hipMemcpyDeviceToDevice, c->stream));
+    KP_HIP(hipMemcpyAsync(c->d.topo, c->h_topo.data(), sizeof(int32_t) * N,
+                          hipMemcpyHostToDevice, c->stream));
+  }
+  KP_HIP(hipStreamSynchronize(c->stream));
+  c->util_scale_loaded = 0;  // force an R rebuild at the next solve
+  c->cap_rows = c->d.score ? c->cap_rows : 0;
+  if (c->d.score) {  // row stride depends on N
+    (void)hipFree(c->d.score);
+    (void)hipFree(c->d.mask);
+    c->d.score = nullptr;
+    c->d.mask = nullptr;
+    c->cap_rows = 0;
+  }
+  c->nodes_loaded = true;
+  c->solved = false;
+  return KP_OK;
+}
+
+int kp_load_jobs(kp_ctx *c, int32_t J, const int64_t *req, const int32_t *prio,
+                 const int32_t *gang_id, const int32_t *gang_size) {
+  if (!c) return KP_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->nodes_loaded) return KP_ESTATE;
+  const int32_t D = c->D;
+  if (J < 0 || (J > 0 && !req)) return KP_EINVAL;
+  for (int64_t i = 0; i < (int64_t)D * J; ++i)
+    if (req[i] < 0 || req[i] > KP_MAX_VALUE) return KP_EINVAL;
+  // units: maximal runs of equal gang_id >= 0 (one CR's replicas); rank order
+  std::vector<int32_t> leader, size, uprio;
+  try {
+    leader.reserve(J);
+    size.reserve(J);
+    uprio.reserve(J);
+    for (int32_t j = 0; j < J;) {
+      const int32_t gid = gang_id ? gang_id[j] : -1;
+      int32_t e = j + 1;
+      if (gid >= 0)
+        while (e < J && gang_id[e] == gid) ++e;
+      const int32_t len = e - j;
+      if (len > KP_MAX_GANG) return KP_EINVAL;
+      for (int32_t k = j; k < e; ++k) {
+        if (gang_size && gang_size[k] != len) return KP_EINVAL;
+        if (prio && prio[k] != prio[j]) return KP_EINVAL;
+        for (int d = 0; d < D; ++d)
+          if (req[(int64_t)d * J + k] != req[(int64_t)d * J + j]) return KP_EINVAL;
+      }
+      leader.push_back(j);
+      size.push_back(len);
+      uprio.push_back(prio ? prio[j] : 0);
+      j = e;
+    }
+    if (gang_id) {  // a gang id may not reappear in a later run
+      std::vector<int32_t> ids;
+      for (size_t u = 0; u < leader.size(); ++u)
+        if (gang_id[leader[u]] >= 0) ids.push_back(gang_id[leader[u]]);
+      std::sort(ids.begin(), ids.end());
+      if (std::adjacent_find(ids.begin(), ids.end()) != ids.end()) return KP_EINVAL;
+    }
+    const int32_t U = (int32_t)leader.size();
+    std::vector<int32_t> ord(U);
+    for (int32_t u = 0; u < U; ++u) ord[u] = u;
+    // leaders ascend with u, so a stable sort on priority gives (prio desc, leader asc)
+    std::stable_sort(ord.begin(), ord.end(),
+                     [&](int32_t a, int32_t b) { return uprio[a] > uprio[b]; });
+    c->h_leader.resize(U);
+    c->h_size.resize(U);
+    c->h_q.resize((size_t)D * U);
+    for (int32_t r = 0; r < U; ++r) {
+      c->h_leader[r] = leader[ord[r]];
+      c->h_size[r] = size[ord[r]];
+      for (int d = 0; d < D; ++d)
+        c->h_q[(size_t)d * U + r] = req[(int64_t)d * J + leader[ord[r]]];
+    }
+    c->J = J;
+    c->U = U;
+  } catch (const std::bad_alloc &) {
+    return KP_ENOMEM;
+  }
+  KP_HIP(hipSetDevice(c->device));
+  KP_TRY(ensure_units(c, c->U, J));
+  KP_TRY(ensure_q(c, c->U, D));
+  if (c->U > 0) {
+    KP_HIP(hipMemcpyAsync(c->d.leader, c->h_leader.data(), sizeof(int32_t) * c->U,
+                          hipMemcpyHostToDevice, c->stream));
+    KP_HIP(hipMemcpyAsync(c->d.size, c->h_size.data(), sizeof(int32_t) * c->U,
+                          hipMemcpyHostToDevice, c->stream));
+    KP_HIP(hipMemcpyAsync(c->d.q, c->h_q.data(), sizeof(int64_t) * D * c->U,
+                          hipMemcpyHostToDevice, c->stream));
+  }
+  KP_HIP(hipStreamSynchronize(c->stream));
+  // this rank's shard: a contiguous block of rank positions
+  c->u_lo = (int32_t)((int64_t)c->U * c->rank / c->world);
+  c->u_hi = (int32_t)((int64_t)c->U * (c->rank + 1) / c->world);
+  c->jobs_loaded = true;
+  c->solved = false;
+  return KP_OK;
+}
+
+// ---------------------------------------------------------------------------
+static int exchange_candidates(kp_ctx *c, int32_t A_local, int32_t K, int32_t *A_global) {
+  ncclComm_t comm = static_cast<ncclComm_t>(c->nccl_comm);
+  c->pinned[0] = A_local;
+  KP_HIP(hipMemcpyAsync(c->d.counters, c->pinned, sizeof(int32_t), hipMemcpyHostToDevice,
+                        c->stream));
+  if (ncclAllGather(c->d.counters, c->d.xg_counts, 1, ncclInt32, comm, c->stream) != ncclSuccess)
+    return KP_ERCCL;
+  KP_HIP(hipMemcpyAsync(c->pinned + 16, c->d.xg_counts, sizeof(int32_t) * c->world,
+                        hipMemcpyDeviceToHost, c->stream));
+  KP_HIP(hipStreamSynchronize(c->stream));
+  int32_t Umax = 0, tot = 0;
+  for (int r = 0; r < c->world; ++r) {
+    Umax = std::max(Umax, c->pinned[16 + r]);
+    tot += c->pinned[16 + r];
+  }
+  *A_global = tot;
+  if (tot == 0) return KP_OK;
+  KP_TRY(launch_pack_exchange(c, A_local, K));
+  if (ncclAllGather(c->d.xg_send, c->d.xg_recv, (size_t)Umax * (K + 1), ncclInt32, comm,
+                    c->stream) != ncclSuccess)
+    return KP_ERCCL;
+  return launch_unpack_exchange(c, c->world, Umax, K, A_global);
+}
+
+static double ev_ms(hipEvent_t a, hipEvent_t b) {
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.0;
+  return ms;
+}
+
+static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
+  KP_TRY(check_params(p, c->D));
+  KP_HIP(hipSetDevice(c->device));
+  const ScoreParams sp = make_sp(c, p);
+  const int32_t K = p->n_cand, U = c->U, N = c->N;
+  const int64_t Ns = (N + 63) & ~63;
+  KP_TRY(prep_for(c, p));
+  // salts of the rotated tie-break
+  {
+    std::vector<uint32_t> salt(U);
+    for (int32_t u = 0; u < U; ++u) salt[u] = fmix32((uint32_t)c->h_leader[u] ^ p->tie_seed);
+    if (U > 0)
+      KP_HIP(hipMemcpyAsync(c->d.salt, salt.data(), sizeof(uint32_t) * U, hipMemcpyHostToDevice,
+                            c->stream));
+    KP_HIP(hipStreamSynchronize(c->stream));
+  }
+  KP_TRY(launch_reset_units(c));
+  const int64_t rpc = rows_per_chunk(c);
+  const int32_t shard = c->u_hi - c->u_lo;
+  KP_TRY(ensure_matrix(c, (int32_t)std::min<int64_t>(std::max(shard, 1), rpc)));
+
+  std::vector<EvPair> evs;
+  auto ev_begin = [&](EvPair &e) -> int {
+    KP_HIP(hipEventCreate(&e.a));
+    KP_HIP(hipEventCreate(&e.b));
+    KP_HIP(hipEventRecord(e.a, c->stream));
+    return KP_OK;
+  };
+  hipEvent_t t0, t1;
+  KP_HIP(hipEventCreate(&t0));
+  KP_HIP(hipEventCreate(&t1));
+  KP_HIP(hipEventRecord(t0, c->stream));
+  std::vector<std::pair<EvPair, int>> kev;  // (events, 0=score 1=select)
+  kp_timing tm{};
+  int64_t pairs = 0;
+  int32_t rounds = 0, passes = 0;
+  while (true) {
+    if (p->max_rounds > 0 && rounds >= p->max_rounds) break;
+    int32_t A_local = 0, A = 0;
+    KP_TRY(launch_active(c, c->u_lo, c->u_hi, &A_local));
+    // candidates of this rank's active units: filter+score pass, then top-K select
+    for (int64_t r0 = 0; r0 < A_local; r0 += rpc) {
+      const int32_t rows = (int32_t)std::min<int64_t>(rpc, A_local - r0);
+      EvPair e1, e2;
+      if (c->profiling) KP_TRY(ev_begin(e1));
+      KP_TRY(launch_score(c, sp, c->d.act_local + r0, rows, c->d.score, c->d.mask, c->d.q, U));
+      if (c->profiling) {
+        KP_HIP(hipEventRecord(e1.b, c->stream));
+        kev.push_back({e1, 0});
+        KP_TRY(ev_begin(e2));
+      }
+      KP_TRY(launch_select(c, sp, c->d.act_local + r0, rows, c->d.score,
+                           c->d.cand_local + r0 * K));
+      if (c->profiling) {
+        KP_HIP(hipEventRecord(e2.b, c->stream));
+        kev.push_back({e2, 1});
+      }
+      tm.score_launches++;
+      tm.score_bytes += (int64_t)rows * Ns * 4 + (int64_t)rows * (Ns / 64) * 8 +
+                        (int64_t)8 * c->D * rows + (int64_t)3 * 8 * c->D * N + 8 * (int64_t)N;
+      tm.select_bytes += (int64_t)rows * Ns * 4 + (int64_t)rows * K * 4;
+    }
+    if (c->world > 1) {
+      KP_TRY(exchange_candidates(c, A_local, K, &A));
+    } else {
+      A = A_local;
+    }
+    if (A == 0) break;
+    pairs += (int64_t)A * N;
+    KP_TRY(launch_open_init(c, A, K));
+    for (int32_t pass = 0; pass < p->max_passes; ++pass) {
+      KP_TRY(launch_plan(c, sp, A, pass));
+      int32_t P = 0;
+      KP_TRY(launch_compact(c, A, K, &P));
+      if (P == 0) break;
+      ++passes;
+      KP_TRY(launch_accept(c, sp, P));
+      KP_TRY(launch_commit(c, sp, P));
+    }
+    ++rounds;
+  }
+  KP_TRY(launch_finalize(c));
+  KP_HIP(hipEventRecord(t1, c->stream));
+  // per-unit status for the stats
+  std::vector<int32_t> status(U);
+  if (U > 0)
+    KP_HIP(hipMemcpyAsync(status.data(), c->d.status, sizeof(int32_t) * U, hipMemcpyDeviceToHost,
+                          c->stream));
+  KP_HIP(hipStreamSynchronize(c->stream));
+  tm.solve_ms = ev_ms(t0, t1);
+  for (auto &ke : kev) {
+    const double ms = ev_ms(ke.first.a, ke.first.b);
+    (ke.second == 0 ? tm.score_ms : tm.select_ms) += ms;
+    (void)hipEventDestroy(ke.first.a);
+    (void)hipEventDestroy(ke.first.b);
+  }
+  (void)hipEventDestroy(t0);
+  (void)hipEventDestroy(t1);
+  tm.accept_ms = tm.solve_ms - tm.score_ms - tm.select_ms;
+  c->timing = tm;
+  int32_t placed = 0;
+  for (int32_t u = 0; u < U; ++u)
+    if (status[u] == kPlaced) placed += c->h_size[u];
+  c->last.rounds = rounds;
+  c->last.passes = passes;
+  c->last.placed_jobs = placed;
+  c->last.unplaced_jobs = c->J - placed;
+  c->last.units = U;
+  c->last.pairs_scored = pairs;
+  if (stats) {
+    stats->rounds = rounds;
+    stats->passes = passes;
+    stats->placed_jobs = placed;
+    stats->unplaced_jobs = c->J - placed;
+    stats->units = U;
+    stats->pairs_scored = pairs;
+  }
+  c->solved = true;
+  return KP_OK;
+}
+
+int kp_solve(kp_ctx *c, const kp_params *p, kp_result *stats) {
+  if (!c) return KP_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->nodes_loaded || !c->jobs_loaded) return KP_ESTATE;
+  try {
+    return solve_impl(c, p, stats);
+  } catch (const std::bad_alloc &) {
+    return KP_ENOMEM;
+  }
+}
+
+static int fetch_impl(kp_ctx *c, kp_result *r) {
+  KP_HIP(hipSetDevice(c->device));
+  const int32_t J = c->J;
+  if (J > 0) {
+    if (r->node_of_job)
+      KP_HIP(hipMemcpyAsync(r->node_of_job, c->d.job_node, sizeof(int32_t) * J,
+                            hipMemcpyDeviceToHost, c->stream));
+    if (r->score_of_job)
+      KP_HIP(hipMemcpyAsync(r->score_of_job, c->d.job_score, sizeof(int32_t) * J,
+                            hipMemcpyDeviceToHost, c->stream));
+    if (r->status_of_job)
+      KP_HIP(hipMemcpyAsync(r->status_of_job, c->d.job_status, sizeof(int32_t) * J,
+                            hipMemcpyDeviceToHost, c->stream));
+  }
+  if (r->used_out && c->N > 0)
+    KP_HIP(hipMemcpyAsync(r->used_out, c->d.used, sizeof(int64_t) * c->D * c->N,
+                          hipMemcpyDeviceToHost, c->stream));
+  KP_HIP(hipStreamSynchronize(c->stream));
+  r->rounds = c->last.rounds;
+  r->passes = c->last.passes;
+  r->placed_jobs = c->last.placed_jobs;
+  r->unplaced_jobs = c->last.unplaced_jobs;
+  r->units = c->last.units;
+  r->pairs_scored = c->last.pairs_scored;
+  return KP_OK;
+}
+
+int kp_fetch(kp_ctx *c, kp_result *r) {
+  if (!c || !r) return KP_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->solved) return KP_ESTATE;
+  return fetch_impl(c, r);
+}
+
+int kp_place(kp_ctx *c, const kp_snapshot *s, const kp_params *p, kp_result *r) {
+  if (!c || !s || !p || !r) return KP_EINVAL;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (check_params(p, s->D) != KP_OK) return KP_EINVAL;
+  }
+  int rc = kp_load_nodes(c, s->N, s->D, s->cap, s->used, s->topo_domain);
+  if (rc) return rc;
+  rc = kp_load_jobs(c, s->J, s->req, s->prio, s->gang_id, s->gang_size);
+  if (rc) return rc;
+  rc = kp_solve(c, p, nullptr);
+  if (rc) return rc;
+  return kp_fetch(c, r);
+}
+
+int kp_apply_delta(kp_ctx *c, const int32_t *node_idx, const int64_t *delta, int32_t K) {
+  if (!c || K < 0 || (K > 0 && (!node_idx || !delta))) return KP_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->nodes_loaded) return KP_ESTATE;
+  KP_HIP(hipSetDevice(c->device));
+  const int32_t N = c->N, D = c->D;
+  std::vector<int64_t> used((size_t)D * N);
+  if (N > 0)
+    KP_HIP(hipMemcpyAsync(used.data(), c->d.used, sizeof(int64_t) * D * N, hipMemcpyDeviceToHost,
+                          c->stream));
+  KP_HIP(hipStreamSynchronize(c->stream));
+  for (int32_t k = 0; k < K; ++k)
+    if (node_idx[k] < 0 || node_idx[k] >= N) return KP_EINVAL;
+  for (int32_t k = 0; k < K; ++k)
+    for (int d = 0; d < D; ++d) {
+      int64_t &u = used[(size_t)d * N + node_idx[k]];
+      const int64_t dv = delta[(int64_t)d * K + k];
+      if (dv > KP_MAX_VALUE || dv < -KP_MAX_VALUE) return KP_EINVAL;
+      u += dv;
+    }
+  for (size_t i = 0; i < used.size(); ++i)
+    if (used[i] < 0 || used[i] > c->h_cap[i]) return KP_EINVAL;
+  if (N > 0)
+    KP_HIP(hipMemcpyAsync(c->d.used, used.data(), sizeof(int64_t) * D * N, hipMemcpyHostToDevice,
+                          c->stream));
+  KP_HIP(hipStreamSynchronize(c->stream));
+  return KP_OK;
+}
+
+int kp_reset_nodes(kp_ctx *c) {
+  if (!c) return KP_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->nodes_loaded) return KP_ESTATE;
+  KP_HIP(hipSetDevice(c->device));
+  if (c->N > 0)
+    KP_HIP(hipMemcpyAsync(c->d.used, c->d.used0, sizeof(int64_t) * c->D * c->N,
+                          hipMemcpyDeviceToDevice, c->stream));
+  return KP_OK;
+}
+
+int kp_score(kp_ctx *c, const kp_params *p, int32_t job_lo, int32_t job_hi, int32_t *score,
+             uint64_t *mask) {
+  if (!c) return KP_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->nodes_loaded || !c->jobs_loaded) return KP_ESTATE;
+  KP_TRY(check_params(p, c->D));
+  if (job_lo < 0 || job_hi > c->J || job_lo > job_hi) return KP_EINVAL;
+  KP_HIP(hipSetDevice(c->device));
+  const int32_t rows = job_hi - job_lo, N = c->N;
+  if (rows == 0 || N == 0) return KP_OK;
+  KP_TRY(prep_for(c, p));
+  const ScoreParams sp = make_sp(c, p);
+  const int64_t Ns = (N + 63) & ~63, words = Ns / 64, uw = (N + 63) / 64;
+  // job -> unit (rank position) map for the requested rows
+  std::vector<int32_t> unit_of(rows);
+  {
+    std::vector<int32_t> u_of_job(c->J);
+    for (int32_t u = 0; u < c->U; ++u)
+      for (int32_t m = 0; m < c->h_size[u]; ++m) u_of_job[c->h_leader[u] + m] = u;
+    for (int32_t r = 0; r < rows; ++r) unit_of[r] = u_of_job[job_lo + r];
+  }
+  const int64_t rpc = std::min<int64_t>(rows_per_chunk(c), std::max(c->cap_U, 1));
+  KP_TRY(ensure_matrix(c, (int32_t)std::min<int64_t>(rows, rpc)));
+  std::vector<int32_t> hs;
+  std::vector<uint64_t> hm;
+  for (int64_t r0 = 0; r0 < rows; r0 += rpc) {
+    const int32_t nr = (int32_t)std::min<int64_t>(rpc, rows - r0);
+    KP_HIP(hipMemcpyAsync(c->d.act_local, unit_of.data() + r0, sizeof(int32_t) * nr,
+                          hipMemcpyHostToDevice, c->stream));
+    KP_TRY(launch_score(c, sp, c->d.act_local, nr, c->d.score, c->d.mask, c->d.q, c->U));
+    hs.resize((size_t)nr * Ns);
+    hm.resize((size_t)nr * words);
+    KP_HIP(hipMemcpyAsync(hs.data(), c->d.score, sizeof(int32_t) * nr * Ns, hipMemcpyDeviceToHost,
+                          c->stream));
+    KP_HIP(hipMemcpyAsync(hm.data(), c->d.mask, sizeof(uint64_t) * nr * words,
+                          hipMemcpyDeviceToHost, c->stream));
+    KP_HIP(hipStreamSynchronize(c->stream));
+    for (int32_t r = 0; r < nr; ++r) {
+      if (score) std::memcpy(score + (r0 + r) * N, hs.data() + (size_t)r * Ns, sizeof(int32_t) * N);
+      if (mask) std::memcpy(mask + (r0 + r) * uw, hm.data() + (size_t)r * words, sizeof(uint64_t) * uw);
+    }
+  }
+  return KP_OK;
+}
+
+int kp_parse_gpu_memory(const char *s, int64_t *mib) {
+  // CRD pattern ^\d+(Gi|Mi)$ (config/crd/bases/ai.ruijie.io_llmservices.yaml:48-51);
+  // the field is optional (omitempty, api/v1/llmservice_types.go:49-51): "" -> 0.
+  if (!s || !mib) return KP_EINVAL;
+  const size_t n = std::strlen(s);
+  if (n == 0) {
+    *mib = 0;
+    return KP_OK;
+  }
+  if (n < 3) return KP_EINVAL;
+  const char *suf = s + n - 2;
+  int64_t mul;
+  if (suf[0] == 'G' && suf[1] == 'i')
+    mul = 1024;
+  else if (suf[0] == 'M' && suf[1] == 'i')
+    mul = 1;
+  else
+    return KP_EINVAL;
+  int64_t v = 0;
+  for (const char *q = s; q < suf; ++q) {
+    if (*q < '0' || *q > '9') return KP_EINVAL;
+    if (v > (INT64_MAX - (*q - '0')) / 10) return KP_EINVAL;
+    v = v * 10 + (*q - '0');
+  }
+  if (v > INT64_MAX / mul) return KP_EINVAL;
+  *mib = v * mul;
+  return KP_OK;
+}
+
+}  // extern "C"

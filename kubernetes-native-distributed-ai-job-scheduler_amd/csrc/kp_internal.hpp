@@ -1,0 +1,144 @@
+// kp_internal.hpp — shared definitions of libkplace (host orchestration +
+// gfx950 kernels). Not part of the ABI; include/kplace.h is.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/kplace.h"
+
+namespace kp {
+
+// Weyl multiplier of the rotated tie-break and its inverse
+// modulo 2^32 (decodes a node index back out of a packed candidate key).
+constexpr uint32_t kTieMul = 0x9E3779B1u;
+constexpr uint32_t inv32(uint32_t a) {
+  uint32_t x = a;  // Newton iteration: x = x * (2 - a x), 5 steps reach 32 bits
+  for (int i = 0; i < 5; ++i) x *= 2u - a * x;
+  return x;
+}
+constexpr uint32_t kTieMulInv = inv32(kTieMul);
+static_assert(kTieMul * kTieMulInv == 1u, "tie multiplier must be invertible");
+
+enum UnitStatus : int32_t { kActive = 0, kPlaced = 1, kNoFit = 2 };
+
+// Scoring constants copied into kernel arguments (wave-uniform -> SGPRs).
+struct ScoreParams {
+  int32_t D;
+  int32_t N;
+  int32_t w[KP_MAX_DIMS];
+  int32_t most_allocated;  // 1 = MostAllocated, 0 = LeastAllocated
+  int32_t gpu_dim;         // -1 = none
+  int32_t w_gpu_fit;
+  int32_t w_spread;
+  int32_t tie_rotated;
+  int32_t n_cand;
+};
+
+// Device buffers of one context. Node table SoA [D][N]; units in rank order.
+struct DevState {
+  // node table (resident across solves; `used` is committed into)
+  int64_t *cap = nullptr, *used = nullptr, *used0 = nullptr;  // used0: as loaded
+  uint64_t *R = nullptr;  // floor(S*2^32/cap), 0 if cap == 0
+  int64_t *base = nullptr;
+  int32_t *topo = nullptr;
+  // units (rank order), job outputs
+  int64_t *q = nullptr;  // [D][U]
+  int32_t *leader = nullptr, *size = nullptr, *status = nullptr;
+  uint32_t *salt = nullptr;
+  int32_t *job_node = nullptr, *job_score = nullptr, *job_status = nullptr;
+  // round scratch
+  int32_t *act = nullptr;       // [U] active unit ids of this round (global order)
+  int32_t *act_local = nullptr; // [U] this rank's active units
+  int32_t *cand = nullptr;      // [U*K] candidate nodes per active slot
+  int32_t *cand_local = nullptr;// [U*K]
+  int32_t *score = nullptr;     // [rows*N] materialised score matrix (chunk)
+  uint64_t *mask = nullptr;     // [rows*ceil(N/64)]
+  uint8_t *open = nullptr;      // [U] per active slot
+  uint8_t *unit_bad = nullptr;  // [U] per unit id
+  // pass scratch: per active slot a staging slab of K proposals
+  int32_t *st_node = nullptr, *st_count = nullptr, *st_off = nullptr, *st_score = nullptr;  // [U*K]
+  int32_t *st_n = nullptr;      // [U] proposals per slot
+  int32_t *st_pos = nullptr;    // [U+1] exclusive scan of st_n
+  // compact proposals (rank order), sorted copies
+  int32_t *p_slot = nullptr, *p_node = nullptr, *p_count = nullptr, *p_off = nullptr, *p_score = nullptr;
+  uint32_t *k_in = nullptr, *k_out = nullptr, *v_in = nullptr, *v_out = nullptr;
+  uint8_t *p_ok = nullptr;
+  int32_t *heads = nullptr;     // segment heads after the sort
+  int32_t *counters = nullptr;  // small device counters
+  void *temp = nullptr;         // rocprim temporary storage
+  size_t temp_bytes = 0;
+  // dist exchange
+  int32_t *xg_counts = nullptr; // [world]
+  int32_t *xg_send = nullptr;   // [Umax*(K+1)]
+  int32_t *xg_recv = nullptr;   // [world*Umax*(K+1)]
+};
+
+}  // namespace kp
+
+struct kp_ctx {
+  std::mutex mu;
+  int device = 0;
+  int world = 1, rank = 0;
+  void *nccl_comm = nullptr;  // ncclComm_t
+  int64_t max_pairs_matrix = 0;
+  hipStream_t stream = nullptr;
+  bool profiling = false;
+  // sizes
+  int32_t N = 0, D = 0, J = 0, U = 0;
+  int32_t cap_N = 0, cap_U = 0, cap_J = 0, cap_rows = 0, cap_props = 0, cap_K = 0;
+  int32_t u_lo = 0, u_hi = 0;  // this rank's shard of units (rank positions)
+  bool nodes_loaded = false, jobs_loaded = false, solved = false;
+  int32_t util_scale_loaded = 0;  // S the R table was built for
+  int32_t mode_loaded = -1;
+  int32_t w_loaded[KP_MAX_DIMS] = {0};
+  // host mirrors
+  std::vector<int64_t> h_cap, h_used;
+  std::vector<int32_t> h_topo;
+  std::vector<int32_t> h_leader, h_size;
+  std::vector<int64_t> h_q;
+  // pinned host scratch
+  int32_t *pinned = nullptr;  // small counters
+  kp::DevState d;
+  kp_result last{};
+  kp_timing timing{};
+  std::string last_error;
+};
+
+// Kernel launchers (kp_kernels.hip).
+namespace kp {
+int launch_prep_nodes(kp_ctx *c, int32_t S, int most_allocated, const int32_t *w);
+int launch_score(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit,
+                 int32_t rows, int32_t *score, uint64_t *mask, const int64_t *q,
+                 int32_t qstride);
+int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit,
+                  int32_t rows, const int32_t *score, int32_t *cand);
+int launch_open_init(kp_ctx *c, int32_t A, int32_t K);
+int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass);
+int launch_compact(kp_ctx *c, int32_t A, int32_t K, int32_t *P_host);
+int launch_accept(kp_ctx *c, const ScoreParams &sp, int32_t P);
+int launch_commit(kp_ctx *c, const ScoreParams &sp, int32_t P);
+int launch_active(kp_ctx *c, int32_t lo, int32_t hi, int32_t *A_host);
+int launch_reset_units(kp_ctx *c);
+int launch_finalize(kp_ctx *c);
+int launch_unpack_exchange(kp_ctx *c, int32_t world, int32_t Umax, int32_t K,
+                           int32_t *A_total);
+int launch_apply_delta(kp_ctx *c, const int32_t *idx, const int64_t *delta,
+                       int32_t K, int32_t *bad);
+size_t rocprim_temp_bytes(int32_t max_items);
+}  // namespace kp
+
+#define KP_HIP(expr)                                                \
+  do {                                                              \
+    hipError_t e_ = (expr);                                         \
+    if (e_ != hipSuccess) {                                         \
+      kp_set_error(#expr, e_);                                      \
+      return KP_EHIP;                                               \
+    }                                                               \
+  } while (0)
+
+void kp_set_error(const char *what, hipError_t e);

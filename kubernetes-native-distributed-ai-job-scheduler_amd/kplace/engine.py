@@ -1,0 +1,180 @@
+"""Thin Python handle over libkplace.so (the product is the C-ABI library).
+
+Every method maps 1:1 onto an entry point of include/kplace.h, with the same
+argument meaning and error behaviour: a negative return code raises
+KPlaceError carrying the code and kp_strerror(). There is no fallback: if the
+shared library or a gfx950 device is missing, construction fails.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _abi
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        _lib = _abi.load_library()
+    return _lib
+
+
+class KPlaceError(RuntimeError):
+    def __init__(self, code: int, where: str):
+        self.code = code
+        msg = lib().kp_strerror(code).decode(errors="replace")
+        super().__init__(f"{where}: kplace error {code} ({msg})")
+
+
+def _check(rc: int, where: str) -> None:
+    if rc != _abi.KP_OK:
+        raise KPlaceError(rc, where)
+
+
+def _ptr(a, t):
+    return None if a is None else a.ctypes.data_as(C.POINTER(t))
+
+
+def _c(a, dt):
+    return None if a is None else np.ascontiguousarray(a, dtype=dt)
+
+
+def default_params_lib() -> _abi.Params:
+    p = _abi.Params()
+    lib().kp_params_default(C.byref(p))
+    return p
+
+
+def unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    _check(lib().kp_dist_unique_id(buf), "kp_dist_unique_id")
+    return buf.raw
+
+
+class Placer:
+    """One kp_ctx: a GPU (one rank of a multi-process job) and its resident
+    node table."""
+
+    def __init__(self, device: int = 0, world_size: int = 1, rank: int = 0,
+                 nccl_id: bytes | None = None, max_pairs_matrix: int = 0):
+        cfg = _abi.Config()
+        cfg.device = device
+        cfg.world_size = world_size
+        cfg.rank = rank
+        self._id = None
+        if nccl_id is not None:
+            self._id = C.create_string_buffer(nccl_id, 128)
+            cfg.nccl_id = C.cast(self._id, C.c_void_p)
+        cfg.max_pairs_matrix = max_pairs_matrix
+        h = C.c_void_p()
+        _check(lib().kp_create(C.byref(h), C.byref(cfg)), "kp_create")
+        self._h = h
+        self.J = self.N = self.D = 0
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().kp_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ---- staged interface -------------------------------------------------
+    def load_nodes(self, cap, used=None, topo=None) -> None:
+        cap = _c(cap, np.int64)
+        D, N = cap.shape
+        used = _c(used, np.int64)
+        topo = _c(topo, np.int32)
+        _check(lib().kp_load_nodes(self._h, N, D, _ptr(cap, C.c_int64), _ptr(used, C.c_int64),
+                                   _ptr(topo, C.c_int32)), "kp_load_nodes")
+        self.N, self.D = N, D
+
+    def load_jobs(self, req, prio=None, gang_id=None, gang_size=None) -> None:
+        req = _c(req, np.int64)
+        J = req.shape[1]
+        prio, gang_id, gang_size = _c(prio, np.int32), _c(gang_id, np.int32), _c(gang_size, np.int32)
+        _check(lib().kp_load_jobs(self._h, J, _ptr(req, C.c_int64), _ptr(prio, C.c_int32),
+                                  _ptr(gang_id, C.c_int32), _ptr(gang_size, C.c_int32)),
+               "kp_load_jobs")
+        self.J = J
+
+    def solve(self, params: _abi.Params) -> dict:
+        r = _abi.Result()
+        _check(lib().kp_solve(self._h, C.byref(params), C.byref(r)), "kp_solve")
+        return dict(rounds=r.rounds, passes=r.passes, placed=r.placed_jobs,
+                    unplaced=r.unplaced_jobs, units=r.units, pairs=r.pairs_scored)
+
+    def fetch(self, want_used: bool = True) -> dict:
+        node = np.empty(self.J, np.int32)
+        score = np.empty(self.J, np.int32)
+        status = np.empty(self.J, np.int32)
+        used = np.empty((self.D, self.N), np.int64) if want_used else None
+        r = _abi.Result(_ptr(node, C.c_int32), _ptr(score, C.c_int32), _ptr(status, C.c_int32),
+                        _ptr(used, C.c_int64))
+        _check(lib().kp_fetch(self._h, C.byref(r)), "kp_fetch")
+        return dict(node=node, score=score, status=status, used=used, rounds=r.rounds,
+                    passes=r.passes, placed=r.placed_jobs, unplaced=r.unplaced_jobs,
+                    units=r.units, pairs=r.pairs_scored)
+
+    def apply_delta(self, node_idx, delta) -> None:
+        node_idx = _c(node_idx, np.int32)
+        delta = _c(delta, np.int64)
+        K = node_idx.shape[0]
+        _check(lib().kp_apply_delta(self._h, _ptr(node_idx, C.c_int32), _ptr(delta, C.c_int64), K),
+               "kp_apply_delta")
+
+    def reset_nodes(self) -> None:
+        _check(lib().kp_reset_nodes(self._h), "kp_reset_nodes")
+
+    def score(self, params: _abi.Params, lo: int, hi: int):
+        rows = hi - lo
+        sc = np.empty((rows, self.N), np.int32)
+        mk = np.empty((rows, (self.N + 63) // 64), np.uint64)
+        _check(lib().kp_score(self._h, C.byref(params), lo, hi, _ptr(sc, C.c_int32),
+                              _ptr(mk, C.c_uint64)), "kp_score")
+        return sc, mk
+
+    def set_profiling(self, on: bool) -> None:
+        _check(lib().kp_set_profiling(self._h, 1 if on else 0), "kp_set_profiling")
+
+    def timing(self) -> dict:
+        t = _abi.Timing()
+        _check(lib().kp_last_timing(self._h, C.byref(t)), "kp_last_timing")
+        return {k: getattr(t, k) for k, _ in _abi.Timing._fields_}
+
+    # ---- one-shot ----------------------------------------------------------
+    def place(self, w, params: _abi.Params) -> dict:
+        """kp_place on a synth.Workload-like object (req/cap/used/prio/gang_id/
+        gang_size/topo attributes)."""
+        req, cap = _c(w.req, np.int64), _c(w.cap, np.int64)
+        D, J = req.shape
+        N = cap.shape[1]
+        used, prio = _c(w.used, np.int64), _c(w.prio, np.int32)
+        gid, gsz, topo = _c(w.gang_id, np.int32), _c(w.gang_size, np.int32), _c(w.topo, np.int32)
+        snap = _abi.Snapshot(J, N, D, _ptr(req, C.c_int64), _ptr(cap, C.c_int64),
+                             _ptr(used, C.c_int64), _ptr(prio, C.c_int32), _ptr(gid, C.c_int32),
+                             _ptr(gsz, C.c_int32), _ptr(topo, C.c_int32))
+        node = np.empty(J, np.int32)
+        score = np.empty(J, np.int32)
+        status = np.empty(J, np.int32)
+        used_out = np.empty((D, N), np.int64)
+        r = _abi.Result(_ptr(node, C.c_int32), _ptr(score, C.c_int32), _ptr(status, C.c_int32),
+                        _ptr(used_out, C.c_int64))
+        _check(lib().kp_place(self._h, C.byref(snap), C.byref(params), C.byref(r)), "kp_place")
+        self.J, self.N, self.D = J, N, D
+        return dict(node=node, score=score, status=status, used=used_out, rounds=r.rounds,
+                    passes=r.passes, placed=r.placed_jobs, unplaced=r.unplaced_jobs,
+                    units=r.units, pairs=r.pairs_scored)

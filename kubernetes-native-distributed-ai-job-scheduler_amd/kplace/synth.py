@@ -1,0 +1,145 @@
+"""Synthetic clusters and pending queues for BASELINE.json configs #2-#5.
+
+Generator contract: splitmix64 with
+seed = 0x6B706C6163650000 + config_no; every draw is lo + (x mod (hi-lo+1))
+on uint64. Draw k of stream s is splitmix64 output number (s << 40) + k + 1
+of that seed, so the whole snapshot is generated with vectorised numpy and is
+identical for any consumer (library, oracle, tests, bench).
+
+Node shapes (x mod 4, or x mod 2 = A/B only for config #3):
+  A 128000 mCPU, 1 TiB, 8 GPU, 8x288 GiB; B 192000, 2 TiB, 8, 8x288 GiB;
+  C 64000, 512 GiB, 0, 0;               D 96000, 768 GiB, 4, 4x192 GiB.
+topo_domain = n // 32 (xGMI island / rack).
+Job (= one replica of an LLMService CR; a CR's replicas = one gang):
+  gpu in {0:40%, 1:30%, 2:15%, 4:10%, 8:5%}; cpu_milli = 1000*[1,32];
+  mem_MiB = 1024*[1,128]; gpu_mem_MiB = gpu*1024*[16,288]; prio in [0,3].
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+GAMMA = np.uint64(0x9E3779B97F4A7C15)
+M1 = np.uint64(0xBF58476D1CE4E5B9)
+M2 = np.uint64(0x94D049BB133111EB)
+SEED_BASE = 0x6B706C6163650000
+
+SHAPES = np.array([
+    [128000, 1048576, 8, 8 * 294912],   # A
+    [192000, 2097152, 8, 8 * 294912],   # B
+    [64000, 524288, 0, 0],              # C
+    [96000, 786432, 4, 4 * 196608],     # D
+], dtype=np.int64)
+
+D = 4  # cpu_milli, mem_MiB, gpu_count, gpu_mem_MiB
+
+
+def splitmix64(seed: int, stream: int, idx: np.ndarray) -> np.ndarray:
+    """splitmix64 output number (stream << 40) + idx + 1 of `seed`."""
+    with np.errstate(over="ignore"):
+        k = (np.uint64(stream) << np.uint64(40)) + idx.astype(np.uint64) + np.uint64(1)
+        z = np.uint64(seed) + k * GAMMA
+        z = (z ^ (z >> np.uint64(30))) * M1
+        z = (z ^ (z >> np.uint64(27))) * M2
+        return z ^ (z >> np.uint64(31))
+
+
+def draw(x: np.ndarray, lo: int, hi: int) -> np.ndarray:
+    return (np.uint64(lo) + x % np.uint64(hi - lo + 1)).astype(np.int64)
+
+
+@dataclass
+class Workload:
+    """One snapshot in the C-ABI's SoA layout (include/kplace.h)."""
+    J: int
+    N: int
+    D: int
+    req: np.ndarray          # int64 [D, J]
+    cap: np.ndarray          # int64 [D, N]
+    used: np.ndarray         # int64 [D, N]
+    prio: np.ndarray         # int32 [J]
+    gang_id: np.ndarray      # int32 [J]
+    gang_size: np.ndarray    # int32 [J]
+    topo: np.ndarray         # int32 [N]
+    name: str = ""
+    meta: dict = field(default_factory=dict)
+
+    def arrays(self):
+        return dict(req=self.req, cap=self.cap, used=self.used, prio=self.prio,
+                    gang_id=self.gang_id, gang_size=self.gang_size, topo=self.topo)
+
+
+def make_nodes(seed: int, N: int, ab_only: bool) -> tuple[np.ndarray, np.ndarray]:
+    x = splitmix64(seed, 0, np.arange(N, dtype=np.uint64))
+    shape = (x % np.uint64(2 if ab_only else 4)).astype(np.int64)
+    cap = SHAPES[shape].T.copy()            # [D, N]
+    topo = (np.arange(N, dtype=np.int64) // 32).astype(np.int32)
+    return np.ascontiguousarray(cap), topo
+
+
+def make_crs(seed: int, n_cr: int, gangs: bool):
+    """Per-CR draws: (size, gpu, cpu, mem, gpu_mem, prio)."""
+    base = np.arange(n_cr, dtype=np.uint64) * np.uint64(8)
+    r = [splitmix64(seed, 1, base + np.uint64(k)) for k in range(6)]
+    size = np.array([1, 2, 4, 8], np.int64)[(r[0] % np.uint64(4)).astype(np.int64)] if gangs \
+        else np.ones(n_cr, np.int64)
+    pct = (r[1] % np.uint64(100)).astype(np.int64)
+    gpu = np.select([pct < 40, pct < 70, pct < 85, pct < 95], [0, 1, 2, 4], 8).astype(np.int64)
+    cpu = 1000 * draw(r[2], 1, 32)
+    mem = 1024 * draw(r[3], 1, 128)
+    gmem = gpu * 1024 * draw(r[4], 16, 288)
+    prio = draw(r[5], 0, 3).astype(np.int32)
+    return size, np.stack([cpu, mem, gpu, gmem]), prio
+
+
+def expand_crs(J: int, size, req_cr, prio_cr, gangs: bool):
+    ends = np.cumsum(size)
+    n_cr = int(np.searchsorted(ends, J, side="left")) + 1
+    size = size[:n_cr].copy()
+    size[-1] -= int(ends[n_cr - 1]) - J          # truncate the last gang to fit J
+    cr_of_job = np.repeat(np.arange(n_cr), size)
+    req = np.ascontiguousarray(req_cr[:, cr_of_job])
+    prio = prio_cr[cr_of_job].astype(np.int32)
+    if gangs:
+        gang_id = cr_of_job.astype(np.int32)
+        gang_size = size[cr_of_job].astype(np.int32)
+    else:
+        gang_id = np.full(J, -1, np.int32)
+        gang_size = np.ones(J, np.int32)
+    return req, prio, gang_id, gang_size
+
+
+def config2(J: int = 10_000, N: int = 1_000) -> Workload:
+    """#2: J x N x 4, used = 0, singletons, bin-pack score only."""
+    seed = SEED_BASE + 2
+    cap, topo = make_nodes(seed, N, ab_only=False)
+    size, req_cr, prio_cr = make_crs(seed, J, gangs=False)
+    req, prio, gid, gsz = expand_crs(J, size, req_cr, prio_cr, gangs=False)
+    return Workload(J, N, D, req, cap, np.zeros_like(cap), prio, gid, gsz, topo,
+                    name=f"config2_{J}x{N}")
+
+
+def config3(J: int = 100_000, N: int = 10_000) -> Workload:
+    """#3: A/B nodes (8-GPU xGMI islands), gangs of {1,2,4,8} replicas."""
+    seed = SEED_BASE + 3
+    cap, topo = make_nodes(seed, N, ab_only=True)
+    size, req_cr, prio_cr = make_crs(seed, J, gangs=True)
+    req, prio, gid, gsz = expand_crs(J, size, req_cr, prio_cr, gangs=True)
+    return Workload(J, N, D, req, cap, np.zeros_like(cap), prio, gid, gsz, topo,
+                    name=f"config3_{J}x{N}")
+
+
+# scoring knobs per config
+CONFIG_PARAMS = {
+    2: dict(w_dim=(1, 1, 1, 1), w_gpu_fit=0, w_spread=0),
+    3: dict(w_dim=(1, 1, 4, 2), w_gpu_fit=1024, w_spread=256),
+}
+
+
+def config(no: int, J: int | None = None, N: int | None = None) -> Workload:
+    if no == 2:
+        return config2(J or 10_000, N or 1_000)
+    if no == 3:
+        return config3(J or 100_000, N or 10_000)
+    raise ValueError(f"config #{no} generator not implemented")

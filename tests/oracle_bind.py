@@ -1,0 +1,128 @@
+"""ctypes binding of the CPU oracle (oracle/libkp_oracle.so).
+
+Test infrastructure only: used by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py as the checker / CPU baseline.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "kubernetes-native-distributed-ai-job-scheduler_amd")
+if PKG not in sys.path:
+    sys.path.insert(0, PKG)
+
+from kplace import _abi  # noqa: E402
+
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "libkp_oracle.so")
+
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            build()
+        L = C.CDLL(ORACLE_SO)
+        vp = C.c_void_p
+        S, P, R = C.POINTER(_abi.Snapshot), C.POINTER(_abi.Params), C.POINTER(_abi.Result)
+        L.kpo_place.argtypes = [S, P, R, C.c_int]
+        L.kpo_score.argtypes = [S, P, C.c_int32, C.c_int32,
+                                C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]
+        L.kpo_state_new.argtypes = [S, P, C.POINTER(vp)]
+        L.kpo_state_free.argtypes = [vp]
+        L.kpo_state_free.restype = None
+        for f in ("kpo_state_units", "kpo_state_active"):
+            getattr(L, f).argtypes = [vp]
+            getattr(L, f).restype = C.c_int32
+        for f in ("kpo_state_unit_leader", "kpo_state_unit_size"):
+            getattr(L, f).argtypes = [vp, C.c_int32]
+            getattr(L, f).restype = C.c_int32
+        L.kpo_round_candidates.argtypes = [vp, C.c_int32, C.c_int32,
+                                           C.POINTER(C.c_int32), C.c_int]
+        L.kpo_round_run.argtypes = [vp, C.POINTER(C.c_int32)]
+        L.kpo_round_run.restype = C.c_int32
+        L.kpo_state_result.argtypes = [vp, R]
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(C.POINTER(t)) if a is not None else None
+
+
+class SnapshotBuf:
+    """Keeps contiguous numpy arrays alive behind a kp_snapshot."""
+
+    def __init__(self, req, cap, used=None, prio=None, gang_id=None, gang_size=None,
+                 topo=None):
+        req = np.ascontiguousarray(req, dtype=np.int64)
+        cap = np.ascontiguousarray(cap, dtype=np.int64)
+        self.D, self.J = req.shape
+        self.N = cap.shape[1]
+        assert cap.shape[0] == self.D
+        self.arrs = dict(
+            req=req, cap=cap,
+            used=None if used is None else np.ascontiguousarray(used, dtype=np.int64),
+            prio=None if prio is None else np.ascontiguousarray(prio, dtype=np.int32),
+            gang_id=None if gang_id is None else np.ascontiguousarray(gang_id, dtype=np.int32),
+            gang_size=None if gang_size is None else np.ascontiguousarray(gang_size, dtype=np.int32),
+            topo=None if topo is None else np.ascontiguousarray(topo, dtype=np.int32),
+        )
+        a = self.arrs
+        self.snap = _abi.Snapshot(
+            self.J, self.N, self.D, _p(a["req"], C.c_int64), _p(a["cap"], C.c_int64),
+            _p(a["used"], C.c_int64), _p(a["prio"], C.c_int32), _p(a["gang_id"], C.c_int32),
+            _p(a["gang_size"], C.c_int32), _p(a["topo"], C.c_int32))
+
+    @classmethod
+    def from_workload(cls, w):
+        return cls(w.req, w.cap, w.used, w.prio, w.gang_id, w.gang_size, w.topo)
+
+
+class ResultBuf:
+    def __init__(self, J, D, N):
+        self.node = np.full(J, -7, np.int32)
+        self.score = np.full(J, -7, np.int32)
+        self.status = np.full(J, -7, np.int32)
+        self.used = np.zeros((D, N), np.int64)
+        self.res = _abi.Result(_p(self.node, C.c_int32), _p(self.score, C.c_int32),
+                               _p(self.status, C.c_int32), _p(self.used, C.c_int64))
+
+    def as_dict(self):
+        r = self.res
+        return dict(node=self.node.copy(), score=self.score.copy(), status=self.status.copy(),
+                    used=self.used.copy(), rounds=r.rounds, passes=r.passes, placed=r.placed_jobs,
+                    unplaced=r.unplaced_jobs, units=r.units, pairs=r.pairs_scored)
+
+
+def place(sb: SnapshotBuf, params, nthreads: int = 1):
+    rb = ResultBuf(sb.J, sb.D, sb.N)
+    rc = lib().kpo_place(C.byref(sb.snap), C.byref(params), C.byref(rb.res), nthreads)
+    if rc != 0:
+        return rc
+    return rb.as_dict()
+
+
+def score(sb: SnapshotBuf, params, lo: int, hi: int):
+    rows = hi - lo
+    words = (sb.N + 63) // 64
+    sc = np.zeros((rows, sb.N), np.int32)
+    mk = np.zeros((rows, words), np.uint64)
+    rc = lib().kpo_score(C.byref(sb.snap), C.byref(params), lo, hi,
+                         _p(sc, C.c_int32), _p(mk, C.c_uint64))
+    if rc != 0:
+        return rc
+    return sc, mk

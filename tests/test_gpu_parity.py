@@ -1,0 +1,255 @@
+"""GPU parity: libkplace.so (HIP, gfx950) against the CPU oracle.
+
+Bar: bit-exact (integer path) — node_of_job, score_of_job, status_of_job,
+used_out and the round/pass counts must equal the oracle's on the same
+seeded snapshot. At BASELINE sizes the oracle still finishes (OpenMP), and
+size-independent properties (capacity, gang all-or-nothing, determinism) are
+checked on top.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from kplace import _abi, synth
+from kplace.engine import KPlaceError, Placer
+
+pytestmark = pytest.mark.gpu
+
+NTH = min(16, os.cpu_count() or 1)
+
+
+def _snap(ob, w):
+    return ob.SnapshotBuf.from_workload(w)
+
+
+def _assert_same(g, o, ctx=""):
+    for k in ("node", "score", "status"):
+        bad = np.nonzero(g[k] != o[k])[0]
+        assert bad.size == 0, f"{ctx} {k} differs at {bad[:10]}: gpu={g[k][bad[:10]]} cpu={o[k][bad[:10]]}"
+    assert np.array_equal(g["used"], o["used"]), f"{ctx} used_out differs"
+    for k in ("rounds", "passes", "placed", "unplaced", "units", "pairs"):
+        assert g[k] == o[k], f"{ctx} {k}: gpu={g[k]} cpu={o[k]}"
+
+
+def random_workload(seed, J, N, D=4, gangs=True, used_frac=0.3, zero_dims=True, max_gang=8,
+                    prio_levels=4):
+    rng = np.random.default_rng(seed)
+    cap = rng.integers(0, 64, size=(D, N)).astype(np.int64) * rng.choice([1, 7, 1000], size=(D, 1))
+    if zero_dims:
+        cap[:, rng.random(N) < 0.1] = 0          # dead nodes
+        cap[rng.integers(0, D), rng.random(N) < 0.2] = 0
+    used = (cap * rng.random((D, N)) * used_frac).astype(np.int64)
+    sizes = []
+    tot = 0
+    while tot < J:
+        s = int(rng.integers(1, max_gang + 1)) if gangs and rng.random() < 0.4 else 1
+        s = min(s, J - tot)
+        sizes.append(s)
+        tot += s
+    sizes = np.array(sizes)
+    ncr = len(sizes)
+    req_cr = (rng.integers(0, 16, size=(D, ncr)) * rng.choice([1, 7, 1000], size=(D, 1))).astype(np.int64)
+    req_cr[:, rng.random(ncr) < 0.05] = 0         # zero-request jobs
+    prio_cr = rng.integers(0, prio_levels, size=ncr).astype(np.int32)
+    cr = np.repeat(np.arange(ncr), sizes)
+    gid = np.where(np.repeat(sizes, sizes) > 1, cr, -1).astype(np.int32) if gangs else np.full(J, -1, np.int32)
+    return synth.Workload(J, N, D, np.ascontiguousarray(req_cr[:, cr]), cap, used,
+                          prio_cr[cr], gid, np.repeat(sizes, sizes).astype(np.int32),
+                          (np.arange(N) // 5).astype(np.int32), name=f"rand{seed}")
+
+
+# ---------------------------------------------------------------------------
+# filter + score matrix (kp_score) — the materialised outputs
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("scale", [100, 1024, 7])
+def test_score_matrix_parity(oracle, placer, mode, scale):
+    w = random_workload(11 + mode + scale, J=300, N=333, gangs=False)
+    p = _abi.default_params(score_mode=mode, util_scale=scale)
+    placer.load_nodes(w.cap, w.used, w.topo)
+    placer.load_jobs(w.req)
+    sc, mk = placer.score(p, 0, w.J)
+    osc, omk = oracle.score(oracle.SnapshotBuf(w.req, w.cap, w.used, topo=w.topo), p, 0, w.J)
+    assert np.array_equal(sc, osc)
+    assert np.array_equal(mk, omk)
+    assert np.array_equal(sc >= 0, np.unpackbits(mk.view(np.uint8), axis=1, bitorder="little")[:, :w.N] == 1)
+
+
+@pytest.mark.parametrize("D", [1, 2, 3, 5, 8])
+def test_score_matrix_dims(oracle, placer, D):
+    w = random_workload(100 + D, J=130, N=200, D=D, gangs=False)
+    p = _abi.default_params(gpu_dim=D - 1, w_dim=[(3 * d + 1) % 7 for d in range(8)])
+    placer.load_nodes(w.cap, w.used, w.topo)
+    placer.load_jobs(w.req)
+    sc, mk = placer.score(p, 5, 120)
+    osc, omk = oracle.score(oracle.SnapshotBuf(w.req, w.cap, w.used, topo=w.topo), p, 5, 120)
+    assert np.array_equal(sc, osc) and np.array_equal(mk, omk)
+
+
+def test_score_matrix_large_values(oracle, placer):
+    # caps beyond 2^32 exercise the 64-bit reciprocal path
+    rng = np.random.default_rng(5)
+    D, N, J = 4, 257, 64
+    cap = rng.integers(1, 1 << 50, size=(D, N), dtype=np.int64)
+    used = (cap // rng.integers(2, 9, size=(D, N))).astype(np.int64)
+    req = rng.integers(0, 1 << 48, size=(D, J), dtype=np.int64)
+    p = _abi.default_params(util_scale=1024)
+    placer.load_nodes(cap, used)
+    placer.load_jobs(req)
+    sc, mk = placer.score(p, 0, J)
+    osc, omk = oracle.score(oracle.SnapshotBuf(req, cap, used), p, 0, J)
+    assert np.array_equal(sc, osc) and np.array_equal(mk, omk)
+
+
+# ---------------------------------------------------------------------------
+# full placement (kp_place)
+# ---------------------------------------------------------------------------
+def _place_both(oracle, placer, w, p):
+    g = placer.place(w, p)
+    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
+    return g, o
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_place_random_parity(oracle, placer, seed):
+    w = random_workload(seed, J=700 + 37 * seed, N=90 + 11 * seed)
+    p = _abi.default_params(tie_mode=seed % 2, score_mode=(seed // 2) % 2,
+                            n_cand=[16, 4, 32, 1, 8, 16][seed], max_passes=[16, 3, 64, 1, 8, 16][seed])
+    g, o = _place_both(oracle, placer, w, p)
+    _assert_same(g, o, f"seed {seed}")
+
+
+def test_place_config2_parity(oracle, placer):
+    w = synth.config2(10_000, 1_000)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[2])
+    g, o = _place_both(oracle, placer, w, p)
+    _assert_same(g, o, "config2")
+
+
+def test_place_config3_small_parity(oracle, placer):
+    w = synth.config3(20_000, 2_000)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[3])
+    g, o = _place_both(oracle, placer, w, p)
+    _assert_same(g, o, "config3 20k")
+
+
+def test_place_config3_full_parity_and_properties(oracle, placer):
+    """BASELINE config #3 at full size: bit-exact + size-independent checks."""
+    w = synth.config3()
+    p = _abi.default_params(**synth.CONFIG_PARAMS[3])
+    g, o = _place_both(oracle, placer, w, p)
+    _assert_same(g, o, "config3 full")
+    _check_properties(w, g)
+    g2 = placer.place(w, p)  # idempotent per snapshot (leader fail-over safety)
+    assert np.array_equal(g2["node"], g["node"]) and np.array_equal(g2["score"], g["score"])
+
+
+def _check_properties(w, g):
+    node = g["node"]
+    placed = node >= 0
+    used = w.used.copy()
+    np.add.at(used.T, node[placed], w.req[:, placed].T)
+    assert np.array_equal(used, g["used"]), "used_out != used + sum of placed requests"
+    assert (g["used"] <= w.cap).all(), "capacity exceeded"
+    # gangs: all members placed or none
+    gid = w.gang_id
+    for g_ in np.unique(gid[gid >= 0])[:2000]:
+        m = placed[gid == g_]
+        assert m.all() or not m.any(), f"gang {g_} partially placed"
+    assert ((g["status"] == 0) == placed).all()
+
+
+def test_place_edge_cases(oracle, placer):
+    p = _abi.default_params()
+    # exact fit: 4 jobs of 2 GPUs on one 8-GPU node, equal scores everywhere
+    cap = np.array([[8], [8], [8], [8]], np.int64)
+    req = np.full((4, 4), 2, np.int64)
+    w = synth.Workload(4, 1, 4, req, cap, np.zeros_like(cap), np.zeros(4, np.int32),
+                       np.full(4, -1, np.int32), np.ones(4, np.int32), np.zeros(1, np.int32))
+    g, o = _place_both(oracle, placer, w, p)
+    _assert_same(g, o, "exact fit")
+    assert (g["node"] == 0).all()
+    # gang larger than the cluster -> NO_FIT, nothing placed
+    req = np.full((4, 3), 5, np.int64)
+    w = synth.Workload(3, 1, 4, req, cap, np.zeros_like(cap), np.zeros(3, np.int32),
+                       np.zeros(3, np.int32), np.full(3, 3, np.int32), np.zeros(1, np.int32))
+    g, o = _place_both(oracle, placer, w, p)
+    _assert_same(g, o, "gang overflow")
+    assert (g["node"] == -1).all() and (g["status"] == _abi.KP_JOB_NO_FIT).all()
+    # many identical nodes, lowest-index tie-break
+    cap = np.full((4, 100), 10, np.int64)
+    req = np.ones((4, 50), np.int64)
+    w = synth.Workload(50, 100, 4, req, cap, np.zeros_like(cap), np.zeros(50, np.int32),
+                       np.full(50, -1, np.int32), np.ones(50, np.int32), np.zeros(100, np.int32))
+    for tie in (0, 1):
+        g, o = _place_both(oracle, placer, w, _abi.default_params(tie_mode=tie))
+        _assert_same(g, o, f"ties {tie}")
+
+
+def test_place_round_limit(oracle, placer):
+    w = synth.config3(5_000, 300)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[3], max_rounds=2)
+    g, o = _place_both(oracle, placer, w, p)
+    _assert_same(g, o, "round limit")
+    assert g["rounds"] == 2 and (g["status"] == _abi.KP_JOB_ROUND_LIMIT).any()
+
+
+def test_place_empty_and_zero_nodes(oracle, placer):
+    p = _abi.default_params()
+    cap = np.full((4, 3), 10, np.int64)
+    w = synth.Workload(0, 3, 4, np.zeros((4, 0), np.int64), cap, np.zeros_like(cap),
+                       np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0, np.int32),
+                       np.zeros(3, np.int32))
+    g, o = _place_both(oracle, placer, w, p)
+    assert g["placed"] == 0 and g["rounds"] == 0 and o["rounds"] == 0
+    w = synth.Workload(5, 0, 4, np.ones((4, 5), np.int64), np.zeros((4, 0), np.int64),
+                       np.zeros((4, 0), np.int64), np.zeros(5, np.int32), np.full(5, -1, np.int32),
+                       np.ones(5, np.int32), np.zeros(0, np.int32))
+    g, o = _place_both(oracle, placer, w, p)
+    _assert_same(g, o, "N=0")
+    assert (g["node"] == -1).all()
+
+
+def test_invalid_inputs_rejected(placer):
+    p = _abi.default_params()
+    cap = np.full((4, 2), 10, np.int64)
+    used = cap + 1  # used > cap
+    with pytest.raises(KPlaceError) as e:
+        placer.load_nodes(cap, used)
+    assert e.value.code == _abi.KP_EINVAL
+    placer.load_nodes(cap)
+    with pytest.raises(KPlaceError):
+        placer.load_jobs(-np.ones((4, 2), np.int64))
+    # gang members with different requests
+    req = np.array([[1, 2]] * 4, np.int64)
+    with pytest.raises(KPlaceError):
+        placer.load_jobs(req, gang_id=np.array([7, 7], np.int32))
+    placer.load_jobs(np.ones((4, 2), np.int64))
+    bad = _abi.default_params(n_cand=0)
+    with pytest.raises(KPlaceError):
+        placer.solve(bad)
+    placer.solve(p)
+
+
+def test_streaming_apply_delta(oracle, placer):
+    """config #5 shape in miniature: micro-batches against a resident table."""
+    w = synth.config2(3_000, 400)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[2])
+    placer.load_nodes(w.cap, w.used, w.topo)
+    used = w.used.copy()
+    rng = np.random.default_rng(3)
+    for b in range(3):
+        lo, hi = b * 1000, (b + 1) * 1000
+        req = np.ascontiguousarray(w.req[:, lo:hi])
+        placer.load_jobs(req, w.prio[lo:hi])
+        placer.solve(p)
+        g = placer.fetch()
+        o = oracle.place(oracle.SnapshotBuf(req, w.cap, used, w.prio[lo:hi], topo=w.topo), p, NTH)
+        _assert_same(g, o, f"batch {b}")
+        used = g["used"].copy()
+        # 20% of the placed jobs complete: negative deltas
+        done = np.nonzero(g["node"] >= 0)[0]
+        done = done[rng.random(done.size) < 0.2]
+        placer.apply_delta(g["node"][done], -req[:, done])
+        np.subtract.at(used.T, g["node"][done], req[:, done].T)
