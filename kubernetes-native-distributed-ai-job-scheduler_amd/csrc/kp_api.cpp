@@ -27,7 +27,7 @@ void kp_set_error(const char *what, hipError_t e) {
 }
 
 namespace kp {
-int launch_pack_exchange(kp_ctx *c, int32_t A, int32_t K);
+
 
 static uint32_t fmix32(uint32_t h) {
   h ^= h >> 16;
@@ -85,7 +85,8 @@ static int ensure_nodes(kp_ctx *c, int32_t N, int32_t D) {
   KP_TRY(dalloc(&c->d.R, (size_t)D * n));
   KP_TRY(dalloc(&c->d.base, (size_t)n));
   KP_TRY(dalloc(&c->d.topo, (size_t)n));
-  KP_TRY(dalloc(&c->d.heads, 2 * (size_t)n));
+  KP_TRY(dalloc(&c->d.seg_start, (size_t)n));
+  KP_TRY(dalloc(&c->d.seg_end, (size_t)n));
   c->cap_N = n;
   return KP_OK;
 }
@@ -101,24 +102,16 @@ static int ensure_units(kp_ctx *c, int32_t U, int32_t J) {
     KP_TRY(dalloc(&c->d.act_local, u));
     KP_TRY(dalloc(&c->d.cand_local, u * K));
     KP_TRY(dalloc(&c->d.open, u));
-    KP_TRY(dalloc(&c->d.unit_bad, u));
-    KP_TRY(dalloc(&c->d.st_node, u * K));
-    KP_TRY(dalloc(&c->d.st_count, u * K));
-    KP_TRY(dalloc(&c->d.st_off, u * K));
-    KP_TRY(dalloc(&c->d.st_score, u * K));
-    KP_TRY(dalloc(&c->d.st_n, u + 1));
-    KP_TRY(dalloc(&c->d.st_pos, u + 1));
-    const size_t pm = u * K;  // max proposals per pass
-    KP_TRY(dalloc(&c->d.p_slot, pm));
-    KP_TRY(dalloc(&c->d.p_node, pm));
-    KP_TRY(dalloc(&c->d.p_count, pm));
-    KP_TRY(dalloc(&c->d.p_off, pm));
-    KP_TRY(dalloc(&c->d.p_score, pm));
-    KP_TRY(dalloc(&c->d.k_in, pm));
-    KP_TRY(dalloc(&c->d.k_out, pm));
-    KP_TRY(dalloc(&c->d.v_in, pm));
-    KP_TRY(dalloc(&c->d.v_out, pm));
-    KP_TRY(dalloc(&c->d.p_ok, pm));
+    KP_TRY(dalloc(&c->d.flag, u));
+    const size_t pm = u * K;  // (slot, candidate) pairs of a round
+    KP_TRY(dalloc(&c->d.planned, pm));
+    KP_TRY(dalloc(&c->d.s0, pm));
+    KP_TRY(dalloc(&c->d.ok, pm));
+    KP_TRY(dalloc(&c->d.csr_kin, pm));
+    KP_TRY(dalloc(&c->d.csr_vin, pm));
+    KP_TRY(dalloc(&c->d.csr_keys, pm));
+    KP_TRY(dalloc(&c->d.csr_vals, pm));
+    KP_TRY(dalloc(&c->d.pass_flag, 64));
     KP_TRY(dalloc(&c->d.counters, 64));
     c->d.temp_bytes = rocprim_temp_bytes((int32_t)std::min<size_t>(pm, INT32_MAX));
     KP_TRY(dalloc(reinterpret_cast<uint8_t **>(&c->d.temp), c->d.temp_bytes));
@@ -296,10 +289,9 @@ void kp_destroy(kp_ctx *c) {
   DevState &d = c->d;
   void *ptrs[] = {d.cap, d.used, d.used0, d.R, d.base, d.topo, d.q, d.leader, d.size, d.status, d.salt,
                   d.job_node, d.job_score, d.job_status, d.act_local, d.cand_local, d.score,
-                  d.mask, d.open, d.unit_bad, d.st_node, d.st_count, d.st_off, d.st_score,
-                  d.st_n, d.st_pos, d.p_slot, d.p_node, d.p_count, d.p_off, d.p_score, d.k_in,
-                  d.k_out, d.v_in, d.v_out, d.p_ok, d.heads, d.counters, d.temp, d.xg_counts,
-                  d.xg_send, d.xg_recv};
+                  d.mask, d.open, d.flag, d.planned, d.s0, d.ok, d.csr_kin, d.csr_vin,
+                  d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
+                  d.temp, d.xg_counts, d.xg_send, d.xg_recv};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->world > 1) {
@@ -479,7 +471,7 @@ static int exchange_candidates(kp_ctx *c, int32_t A_local, int32_t K, int32_t *A
   if (ncclAllGather(c->d.xg_send, c->d.xg_recv, (size_t)Umax * (K + 1), ncclInt32, comm,
                     c->stream) != ncclSuccess)
     return KP_ERCCL;
-  return launch_unpack_exchange(c, c->world, Umax, K, A_global);
+  return launch_unpack_exchange(c, c->world, Umax, K);
 }
 
 static double ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -524,10 +516,20 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   kp_timing tm{};
   int64_t pairs = 0;
   int32_t rounds = 0, passes = 0;
+  // pass flags of the previous round land in pinned memory; they are counted
+  // after the next stream synchronisation (no extra round trip per round)
+  int32_t *flags_h = c->pinned + 512;
+  bool flags_pending = false;
+  auto count_flags = [&]() {
+    if (!flags_pending) return;
+    for (int i = 0; i < p->max_passes; ++i) passes += flags_h[i] != 0;
+    flags_pending = false;
+  };
   while (true) {
     if (p->max_rounds > 0 && rounds >= p->max_rounds) break;
     int32_t A_local = 0, A = 0;
     KP_TRY(launch_active(c, c->u_lo, c->u_hi, &A_local));
+    count_flags();
     // candidates of this rank's active units: filter+score pass, then top-K select
     for (int64_t r0 = 0; r0 < A_local; r0 += rpc) {
       const int32_t rows = (int32_t)std::min<int64_t>(rpc, A_local - r0);
@@ -558,15 +560,17 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     if (A == 0) break;
     pairs += (int64_t)A * N;
     KP_TRY(launch_open_init(c, A, K));
+    KP_TRY(launch_csr_build(c, A, K));
+    KP_HIP(hipMemsetAsync(c->d.pass_flag, 0, sizeof(int32_t) * 64, c->stream));
+    // passes run back to back on the device: no host round trip inside a round
     for (int32_t pass = 0; pass < p->max_passes; ++pass) {
       KP_TRY(launch_plan(c, sp, A, pass));
-      int32_t P = 0;
-      KP_TRY(launch_compact(c, A, K, &P));
-      if (P == 0) break;
-      ++passes;
-      KP_TRY(launch_accept(c, sp, P));
-      KP_TRY(launch_commit(c, sp, P));
+      KP_TRY(launch_accept(c, sp));
+      KP_TRY(launch_commit(c, sp, A));
     }
+    KP_HIP(hipMemcpyAsync(flags_h, c->d.pass_flag, sizeof(int32_t) * 64, hipMemcpyDeviceToHost,
+                          c->stream));
+    flags_pending = true;
     ++rounds;
   }
   KP_TRY(launch_finalize(c));
@@ -577,6 +581,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     KP_HIP(hipMemcpyAsync(status.data(), c->d.status, sizeof(int32_t) * U, hipMemcpyDeviceToHost,
                           c->stream));
   KP_HIP(hipStreamSynchronize(c->stream));
+  count_flags();
   tm.solve_ms = ev_ms(t0, t1);
   for (auto &ke : kev) {
     const double ms = ev_ms(ke.first.a, ke.first.b);

@@ -59,16 +59,15 @@ struct DevState {
   int32_t *score = nullptr;     // [rows*N] materialised score matrix (chunk)
   uint64_t *mask = nullptr;     // [rows*ceil(N/64)]
   uint8_t *open = nullptr;      // [U] per active slot
-  uint8_t *unit_bad = nullptr;  // [U] per unit id
-  // pass scratch: per active slot a staging slab of K proposals
-  int32_t *st_node = nullptr, *st_count = nullptr, *st_off = nullptr, *st_score = nullptr;  // [U*K]
-  int32_t *st_n = nullptr;      // [U] proposals per slot
-  int32_t *st_pos = nullptr;    // [U+1] exclusive scan of st_n
-  // compact proposals (rank order), sorted copies
-  int32_t *p_slot = nullptr, *p_node = nullptr, *p_count = nullptr, *p_off = nullptr, *p_score = nullptr;
-  uint32_t *k_in = nullptr, *k_out = nullptr, *v_in = nullptr, *v_out = nullptr;
-  uint8_t *p_ok = nullptr;
-  int32_t *heads = nullptr;     // segment heads after the sort
+  int32_t *flag = nullptr;      // [U] active flags (compaction input)
+  // pass state per (active slot, candidate): members planned / pass-start
+  // score / accepted
+  int32_t *planned = nullptr, *s0 = nullptr;  // [U*K]
+  uint8_t *ok = nullptr;                      // [U*K]
+  // node -> (slot, candidate) inverse index, rebuilt once per round
+  uint32_t *csr_kin = nullptr, *csr_vin = nullptr, *csr_keys = nullptr, *csr_vals = nullptr;
+  int32_t *seg_start = nullptr, *seg_end = nullptr;  // [N]
+  int32_t *pass_flag = nullptr; // [64] pass p produced proposals
   int32_t *counters = nullptr;  // small device counters
   void *temp = nullptr;         // rocprim temporary storage
   size_t temp_bytes = 0;
@@ -118,17 +117,15 @@ int launch_score(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit,
 int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit,
                   int32_t rows, const int32_t *score, int32_t *cand);
 int launch_open_init(kp_ctx *c, int32_t A, int32_t K);
+int launch_csr_build(kp_ctx *c, int32_t A, int32_t K);
 int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass);
-int launch_compact(kp_ctx *c, int32_t A, int32_t K, int32_t *P_host);
-int launch_accept(kp_ctx *c, const ScoreParams &sp, int32_t P);
-int launch_commit(kp_ctx *c, const ScoreParams &sp, int32_t P);
+int launch_accept(kp_ctx *c, const ScoreParams &sp);
+int launch_commit(kp_ctx *c, const ScoreParams &sp, int32_t A);
 int launch_active(kp_ctx *c, int32_t lo, int32_t hi, int32_t *A_host);
 int launch_reset_units(kp_ctx *c);
 int launch_finalize(kp_ctx *c);
-int launch_unpack_exchange(kp_ctx *c, int32_t world, int32_t Umax, int32_t K,
-                           int32_t *A_total);
-int launch_apply_delta(kp_ctx *c, const int32_t *idx, const int64_t *delta,
-                       int32_t K, int32_t *bad);
+int launch_pack_exchange(kp_ctx *c, int32_t A, int32_t K);
+int launch_unpack_exchange(kp_ctx *c, int32_t world, int32_t Umax, int32_t K);
 size_t rocprim_temp_bytes(int32_t max_items);
 }  // namespace kp
 
