@@ -104,9 +104,16 @@ static int ensure_units(kp_ctx *c, int32_t U, int32_t J) {
     KP_TRY(dalloc(&c->d.open, u));
     KP_TRY(dalloc(&c->d.flag, u));
     const size_t pm = u * K;  // (slot, candidate) pairs of a round
-    KP_TRY(dalloc(&c->d.planned, pm));
     KP_TRY(dalloc(&c->d.s0, pm));
+    KP_TRY(dalloc(&c->d.bid, pm));
     KP_TRY(dalloc(&c->d.ok, pm));
+    KP_TRY(dalloc(&c->d.win, pm / 64 + 128));
+    KP_TRY(dalloc(&c->d.inv, pm));
+    KP_TRY(dalloc(&c->d.ent_unit, pm));
+    KP_TRY(dalloc(&c->d.ent_slot, pm));
+    KP_TRY(dalloc(&c->d.ent_size, pm));
+    KP_TRY(dalloc(&c->d.ent_lead, pm));
+    KP_TRY(dalloc(&c->d.ent_q, pm * KP_MAX_DIMS));
     KP_TRY(dalloc(&c->d.csr_kin, pm));
     KP_TRY(dalloc(&c->d.csr_vin, pm));
     KP_TRY(dalloc(&c->d.csr_keys, pm));
@@ -289,7 +296,9 @@ void kp_destroy(kp_ctx *c) {
   DevState &d = c->d;
   void *ptrs[] = {d.cap, d.used, d.used0, d.R, d.base, d.topo, d.q, d.leader, d.size, d.status, d.salt,
                   d.job_node, d.job_score, d.job_status, d.act_local, d.cand_local, d.score,
-                  d.mask, d.open, d.flag, d.planned, d.s0, d.ok, d.csr_kin, d.csr_vin,
+                  d.mask, d.open, d.flag, d.s0, d.bid, d.ok, d.win, d.inv, d.ent_unit,
+                  d.ent_slot, d.ent_size, d.ent_lead, d.ent_q,
+                  d.csr_kin, d.csr_vin,
                   d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
                   d.temp, d.xg_counts, d.xg_send, d.xg_recv};
   for (void *p : ptrs)
@@ -341,6 +350,9 @@ int kp_load_nodes(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap, const int
     return KP_ENOMEM;
   }
   if (D != c->D) c->jobs_loaded = false;  // request layout depends on D
+  c->caps32 = true;
+  for (int64_t i = 0; i < (int64_t)D * N; ++i) c->caps32 = c->caps32 && cap[i] < ((int64_t)1 << 32);
+  c->fits32 = c->caps32 && c->reqs32 && c->jobs_loaded;
   KP_TRY(ensure_nodes(c, N, D));
   c->N = N;
   c->D = D;
@@ -444,7 +456,10 @@ int kp_load_jobs(kp_ctx *c, int32_t J, const int64_t *req, const int32_t *prio,
   // this rank's shard: a contiguous block of rank positions
   c->u_lo = (int32_t)((int64_t)c->U * c->rank / c->world);
   c->u_hi = (int32_t)((int64_t)c->U * (c->rank + 1) / c->world);
+  c->reqs32 = true;
+  for (int64_t i = 0; i < (int64_t)D * J; ++i) c->reqs32 = c->reqs32 && req[i] < ((int64_t)1 << 32);
   c->jobs_loaded = true;
+  c->fits32 = c->caps32 && c->reqs32;
   c->solved = false;
   return KP_OK;
 }
@@ -565,8 +580,8 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     // passes run back to back on the device: no host round trip inside a round
     for (int32_t pass = 0; pass < p->max_passes; ++pass) {
       KP_TRY(launch_plan(c, sp, A, pass));
-      KP_TRY(launch_accept(c, sp));
-      KP_TRY(launch_commit(c, sp, A));
+      KP_TRY(launch_accept(c, sp, pass, A));
+      KP_TRY(launch_gang_commit(c, sp, A, pass));
     }
     KP_HIP(hipMemcpyAsync(flags_h, c->d.pass_flag, sizeof(int32_t) * 64, hipMemcpyDeviceToHost,
                           c->stream));

@@ -60,12 +60,19 @@ struct DevState {
   uint64_t *mask = nullptr;     // [rows*ceil(N/64)]
   uint8_t *open = nullptr;      // [U] per active slot
   int32_t *flag = nullptr;      // [U] active flags (compaction input)
-  // pass state per (active slot, candidate): members planned / pass-start
-  // score / accepted
-  int32_t *planned = nullptr, *s0 = nullptr;  // [U*K]
-  uint8_t *ok = nullptr;                      // [U*K]
+  // pass state: pass-start score per (slot, candidate); per bidder entry e
+  // (node-sorted order) a pass-tagged bid and the gang accept bit; a flag per
+  // 64-entry window
+  int32_t *s0 = nullptr;        // [U*K]
+  uint32_t *bid = nullptr;      // [U*K] (pass << 8) | members
+  uint8_t *ok = nullptr;        // [U*K]
+  int32_t *win = nullptr;       // [U*K/64 + 64]
   // node -> (slot, candidate) inverse index, rebuilt once per round
   uint32_t *csr_kin = nullptr, *csr_vin = nullptr, *csr_keys = nullptr, *csr_vals = nullptr;
+  int32_t *inv = nullptr;       // [U*K] (slot, candidate) -> entry
+  int32_t *ent_unit = nullptr;  // [U*K] entry -> unit id
+  int32_t *ent_slot = nullptr, *ent_size = nullptr, *ent_lead = nullptr;  // [U*K]
+  int64_t *ent_q = nullptr;     // [D][U*K] request of the entry's unit
   int32_t *seg_start = nullptr, *seg_end = nullptr;  // [N]
   int32_t *pass_flag = nullptr; // [64] pass p produced proposals
   int32_t *counters = nullptr;  // small device counters
@@ -92,6 +99,8 @@ struct kp_ctx {
   int32_t cap_N = 0, cap_U = 0, cap_J = 0, cap_rows = 0, cap_props = 0, cap_K = 0;
   int32_t u_lo = 0, u_hi = 0;  // this rank's shard of units (rank positions)
   bool nodes_loaded = false, jobs_loaded = false, solved = false;
+  // every cap and every req < 2^32: the filter+score pass may run in 32-bit
+  bool caps32 = false, reqs32 = false, fits32 = false;
   int32_t util_scale_loaded = 0;  // S the R table was built for
   int32_t mode_loaded = -1;
   int32_t w_loaded[KP_MAX_DIMS] = {0};
@@ -119,8 +128,8 @@ int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit,
 int launch_open_init(kp_ctx *c, int32_t A, int32_t K);
 int launch_csr_build(kp_ctx *c, int32_t A, int32_t K);
 int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass);
-int launch_accept(kp_ctx *c, const ScoreParams &sp);
-int launch_commit(kp_ctx *c, const ScoreParams &sp, int32_t A);
+int launch_accept(kp_ctx *c, const ScoreParams &sp, int32_t pass, int32_t A);
+int launch_gang_commit(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass);
 int launch_active(kp_ctx *c, int32_t lo, int32_t hi, int32_t *A_host);
 int launch_reset_units(kp_ctx *c);
 int launch_finalize(kp_ctx *c);

@@ -99,6 +99,76 @@ __global__ __launch_bounds__(256) void k_score(ScoreParams sp,
   }
 }
 
+// 32-bit specialisation, chosen by the host when every cap and req is < 2^32
+// (then used+q <= cap < 2^32 on every feasible pair). Same result bit for bit:
+// util = ((u * R) >> 32) with R = Rh*2^32 + Rl (Rh <= S) is
+// mulhi(u, Rl) + u*Rh exactly, since u*Rh*2^32 is a multiple of 2^32.
+// Halves the VALU work per pair so the kernel stays on the HBM store roof.
+template <int D, int NPL>
+__global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
+                                                 const int64_t *__restrict__ cap,
+                                                 const int64_t *__restrict__ used,
+                                                 const uint64_t *__restrict__ R,
+                                                 const int64_t *__restrict__ base,
+                                                 const int64_t *__restrict__ q, int32_t qstride,
+                                                 const int32_t *__restrict__ rows_unit,
+                                                 int32_t rows, int32_t rows_per_block,
+                                                 int32_t *__restrict__ score,
+                                                 uint64_t *__restrict__ mask, int32_t Ns) {
+  const int N = sp.N;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tile0 = blockIdx.x * (256 * NPL) + wave * (64 * NPL);
+  uint32_t f_[NPL][D], u_[NPL][D], rl_[NPL][D], rh_[NPL][D];
+  int32_t b_[NPL];
+  bool v_[NPL];
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) {
+    const int n = tile0 + k * 64 + lane;
+    v_[k] = n < N;
+    const int nn = v_[k] ? n : 0;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int64_t cc = cap[(int64_t)d * N + nn], uu = used[(int64_t)d * N + nn];
+      const uint64_t rr = R[(int64_t)d * N + nn];
+      f_[k][d] = (uint32_t)(cc - uu);
+      u_[k][d] = (uint32_t)uu;
+      rl_[k][d] = (uint32_t)rr;
+      rh_[k][d] = (uint32_t)(rr >> 32);
+    }
+    b_[k] = (int32_t)base[nn];
+  }
+  const int words = Ns >> 6;
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  if (tile0 >= Ns) return;
+  for (int r = r0; r < r1; ++r) {
+    const int32_t unit = rows_unit[r];
+    uint32_t qq[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) qq[d] = (uint32_t)q[(int64_t)d * qstride + unit];
+    int32_t *srow = score + (int64_t)r * Ns;
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const int n = tile0 + k * 64 + lane;
+      bool fits = v_[k];
+      int32_t acc = 0, fit_bonus = 0;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        fits &= qq[d] <= f_[k][d];
+        const uint32_t uu = u_[k][d] + qq[d];
+        const uint32_t util = __umulhi(uu, rl_[k][d]) + uu * rh_[k][d];
+        acc += sp.w[d] * (int32_t)util;
+        if (d == sp.gpu_dim && qq[d] > 0 && f_[k][d] == qq[d]) fit_bonus = sp.w_gpu_fit;
+      }
+      const int32_t s = (sp.most_allocated ? acc : b_[k] - acc) + fit_bonus;
+      if (score && n < Ns) srow[n] = fits ? s : KP_SCORE_INFEASIBLE;
+      const uint64_t bits = __ballot(fits);
+      if (mask && lane == 0 && (tile0 + k * 64) < Ns)
+        mask[(int64_t)r * words + ((tile0 + k * 64) >> 6)] = bits;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // top-K select: one wave per score-matrix row. Each lane keeps its own
 // descending top-KC list of packed keys (valid bit | score | ~tie key) over a
@@ -129,9 +199,12 @@ __global__ __launch_bounds__(256) void k_select(ScoreParams sp,
                                                 const int32_t *__restrict__ rows_unit,
                                                 const uint32_t *__restrict__ salt,
                                                 int32_t rows, int32_t *__restrict__ cand) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
+  // one 256-thread workgroup per row: 4 waves split the row, each wave merges
+  // its lanes' lists, wave 0 merges the 4 wave lists from LDS
+  __shared__ uint64_t part[4][KC];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row = blockIdx.x;
+  if (row >= rows) return;  // block-uniform
   const int K = sp.n_cand;
   const int32_t unit = rows_unit[row];
   const uint32_t sl = sp.tie_rotated ? salt[unit] : 0u;
@@ -141,17 +214,48 @@ __global__ __launch_bounds__(256) void k_select(ScoreParams sp,
   for (int i = 0; i < KC; ++i) k[i] = 0;
   const int4 *row4 = reinterpret_cast<const int4 *>(score + (int64_t)row * Ns);
   const int n4 = Ns >> 2;
-  for (int i = lane; i < n4; i += 64) {
-    const int4 v = row4[i];
-    const int n = i * 4;
-    if (v.x >= 0) topk_insert<KC>(k, pack_key(v.x, (uint32_t)(n + 0) * mul + sl));
-    if (v.y >= 0) topk_insert<KC>(k, pack_key(v.y, (uint32_t)(n + 1) * mul + sl));
-    if (v.z >= 0) topk_insert<KC>(k, pack_key(v.z, (uint32_t)(n + 2) * mul + sl));
-    if (v.w >= 0) topk_insert<KC>(k, pack_key(v.w, (uint32_t)(n + 3) * mul + sl));
+  // 4 independent 16-B loads in flight per lane before any is consumed
+  constexpr int UNR = 4;
+  for (int i0 = threadIdx.x; i0 < n4; i0 += 256 * UNR) {
+    int4 v[UNR];
+#pragma unroll
+    for (int t = 0; t < UNR; ++t) {
+      const int i = i0 + 256 * t;
+      v[t] = i < n4 ? row4[i] : make_int4(-1, -1, -1, -1);
+    }
+#pragma unroll
+    for (int t = 0; t < UNR; ++t) {
+      const int n = (i0 + 256 * t) * 4;
+      if (v[t].x >= 0) topk_insert<KC>(k, pack_key(v[t].x, (uint32_t)(n + 0) * mul + sl));
+      if (v[t].y >= 0) topk_insert<KC>(k, pack_key(v[t].y, (uint32_t)(n + 1) * mul + sl));
+      if (v[t].z >= 0) topk_insert<KC>(k, pack_key(v[t].z, (uint32_t)(n + 2) * mul + sl));
+      if (v[t].w >= 0) topk_insert<KC>(k, pack_key(v[t].w, (uint32_t)(n + 3) * mul + sl));
+    }
+  }
+  // wave merge: K times the wave max of the lanes' heads; its owner pops
+  for (int it = 0; it < K; ++it) {
+    const uint64_t m = wave_max_u64(k[0]);
+    if (lane == 0) part[wave][it] = m;
+    if (m != 0 && k[0] == m) {  // keys are unique per node: exactly one lane pops
+#pragma unroll
+      for (int i = 0; i < KC - 1; ++i) k[i] = k[i + 1];
+      k[KC - 1] = 0;
+    }
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  // block merge: lane l holds entries l and l+64 of the 4*K wave results
+  const int tot = 4 * K;
+  uint64_t h0 = lane < tot ? part[lane / K][lane % K] : 0;
+  uint64_t h1 = lane + 64 < tot ? part[(lane + 64) / K][(lane + 64) % K] : 0;
+  if (h1 > h0) {
+    const uint64_t t = h0;
+    h0 = h1;
+    h1 = t;
   }
   const uint32_t inv = sp.tie_rotated ? kTieMulInv : 1u;
   for (int it = 0; it < K; ++it) {
-    const uint64_t m = wave_max_u64(k[0]);
+    const uint64_t m = wave_max_u64(h0);
     if (lane == 0) {
       int32_t node = -1;
       if (m != 0) {
@@ -160,10 +264,9 @@ __global__ __launch_bounds__(256) void k_select(ScoreParams sp,
       }
       cand[(int64_t)row * K + it] = node;
     }
-    if (m != 0 && k[0] == m) {  // unique keys: exactly one lane pops
-#pragma unroll
-      for (int i = 0; i < KC - 1; ++i) k[i] = k[i + 1];
-      k[KC - 1] = 0;
+    if (m != 0 && h0 == m) {
+      h0 = h1;
+      h1 = 0;
     }
   }
 }
@@ -245,13 +348,21 @@ template <int D>
 struct ScoreL {
   static int run(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
                  int32_t *score, uint64_t *mask, const int64_t *q, int32_t qstride) {
-    constexpr int NPL = D <= 4 ? 2 : 1;
     const int Ns = (c->N + 63) & ~63;
     const int rpb = 32;
-    dim3 grid(blocks(Ns, 256 * NPL), blocks(rows, rpb));
-    hipLaunchKernelGGL((k_score<D, NPL>), grid, dim3(256), 0, c->stream, sp, c->d.cap,
-                       c->d.used, c->d.R, c->d.base, q, qstride, rows_unit, rows, rpb, score,
-                       mask, Ns);
+    if (c->fits32) {
+      constexpr int NPL = D <= 4 ? 4 : 2;
+      dim3 grid(blocks(Ns, 256 * NPL), blocks(rows, rpb));
+      hipLaunchKernelGGL((k_score32<D, NPL>), grid, dim3(256), 0, c->stream, sp, c->d.cap,
+                         c->d.used, c->d.R, c->d.base, q, qstride, rows_unit, rows, rpb, score,
+                         mask, Ns);
+    } else {
+      constexpr int NPL = D <= 4 ? 2 : 1;
+      dim3 grid(blocks(Ns, 256 * NPL), blocks(rows, rpb));
+      hipLaunchKernelGGL((k_score<D, NPL>), grid, dim3(256), 0, c->stream, sp, c->d.cap,
+                         c->d.used, c->d.R, c->d.base, q, qstride, rows_unit, rows, rpb, score,
+                         mask, Ns);
+    }
     KP_HIP(hipGetLastError());
     return KP_OK;
   }
@@ -282,7 +393,7 @@ int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, in
                   const int32_t *score, int32_t *cand) {
   if (rows <= 0) return KP_OK;
   const int Ns = (c->N + 63) & ~63;
-  dim3 grid(blocks(rows, 4)), blk(256);
+  dim3 grid(rows), blk(256);  // one workgroup per row
   const int K = sp.n_cand;
   if (K <= 4)
     hipLaunchKernelGGL(k_select<4>, grid, blk, 0, c->stream, sp, score, Ns, rows_unit, c->d.salt, rows, cand);
