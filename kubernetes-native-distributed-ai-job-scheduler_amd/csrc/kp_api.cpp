@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 
@@ -106,7 +107,9 @@ static int ensure_units(kp_ctx *c, int32_t U, int32_t J) {
     const size_t pm = u * K;  // (slot, candidate) pairs of a round
     KP_TRY(dalloc(&c->d.s0, pm));
     KP_TRY(dalloc(&c->d.bid, pm));
-    KP_TRY(dalloc(&c->d.ok, pm));
+    KP_TRY(dalloc(&c->d.gpart, pm));
+    KP_TRY(dalloc(&c->d.nparts, u));
+    KP_TRY(dalloc(&c->d.arrive, u));
     KP_TRY(dalloc(&c->d.win, pm / 64 + 128));
     KP_TRY(dalloc(&c->d.inv, pm));
     KP_TRY(dalloc(&c->d.ent_unit, pm));
@@ -267,6 +270,8 @@ int kp_create(kp_ctx **out, const kp_config *cfg) {
   c->world = cfg->world_size;
   c->rank = cfg->rank;
   c->max_pairs_matrix = cfg->max_pairs_matrix;
+  if (const char *e = std::getenv("KP_SELECT_LDS_CAP")) c->select_lds_cap = std::atoi(e);
+  if (const char *e = std::getenv("KP_SELECT_GENERIC")) c->select_generic = std::atoi(e) != 0;
   if (hipSetDevice(dev) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void **>(&c->pinned), 4096, hipHostMallocDefault) !=
@@ -296,7 +301,8 @@ void kp_destroy(kp_ctx *c) {
   DevState &d = c->d;
   void *ptrs[] = {d.cap, d.used, d.used0, d.R, d.base, d.topo, d.q, d.leader, d.size, d.status, d.salt,
                   d.job_node, d.job_score, d.job_status, d.act_local, d.cand_local, d.score,
-                  d.mask, d.open, d.flag, d.s0, d.bid, d.ok, d.win, d.inv, d.ent_unit,
+                  d.mask, d.open, d.flag, d.s0, d.bid, d.gpart, d.nparts, d.arrive, d.win,
+                  d.inv, d.ent_unit,
                   d.ent_slot, d.ent_size, d.ent_lead, d.ent_q,
                   d.csr_kin, d.csr_vin,
                   d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
@@ -575,13 +581,11 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     if (A == 0) break;
     pairs += (int64_t)A * N;
     KP_TRY(launch_open_init(c, A, K));
-    KP_TRY(launch_csr_build(c, A, K));
-    KP_HIP(hipMemsetAsync(c->d.pass_flag, 0, sizeof(int32_t) * 64, c->stream));
+    KP_TRY(launch_csr_build(c, A, K));  // also clears the round's pass flags
     // passes run back to back on the device: no host round trip inside a round
     for (int32_t pass = 0; pass < p->max_passes; ++pass) {
       KP_TRY(launch_plan(c, sp, A, pass));
       KP_TRY(launch_accept(c, sp, pass, A));
-      KP_TRY(launch_gang_commit(c, sp, A, pass));
     }
     KP_HIP(hipMemcpyAsync(flags_h, c->d.pass_flag, sizeof(int32_t) * 64, hipMemcpyDeviceToHost,
                           c->stream));

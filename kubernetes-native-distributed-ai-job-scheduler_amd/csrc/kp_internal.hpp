@@ -60,13 +60,16 @@ struct DevState {
   uint64_t *mask = nullptr;     // [rows*ceil(N/64)]
   uint8_t *open = nullptr;      // [U] per active slot
   int32_t *flag = nullptr;      // [U] active flags (compaction input)
-  // pass state: pass-start score per (slot, candidate); per bidder entry e
-  // (node-sorted order) a pass-tagged bid and the gang accept bit; a flag per
-  // 64-entry window
+  // pass state: per bidder entry e (node-sorted order) the pass-start score and
+  // a pass-tagged bid; a flag per 64-entry window; per multi-node gang slot its
+  // parts {node, members, member offset, score} in candidate order, the part
+  // count and an arrival counter (the last accepted part commits the gang)
   int32_t *s0 = nullptr;        // [U*K]
   uint32_t *bid = nullptr;      // [U*K] (pass << 8) | members
-  uint8_t *ok = nullptr;        // [U*K]
   int32_t *win = nullptr;       // [U*K/64 + 64]
+  int4 *gpart = nullptr;        // [U*K]
+  int32_t *nparts = nullptr;    // [U]
+  int32_t *arrive = nullptr;    // [U]
   // node -> (slot, candidate) inverse index, rebuilt once per round
   uint32_t *csr_kin = nullptr, *csr_vin = nullptr, *csr_keys = nullptr, *csr_vals = nullptr;
   int32_t *inv = nullptr;       // [U*K] (slot, candidate) -> entry
@@ -94,6 +97,12 @@ struct kp_ctx {
   int64_t max_pairs_matrix = 0;
   hipStream_t stream = nullptr;
   bool profiling = false;
+  // test knobs, read from the environment at kp_create (never set in
+  // production): KP_SELECT_LDS_CAP shrinks the threshold select's survivor
+  // buffer (forces its threshold-raise path), KP_SELECT_GENERIC=1 forces the
+  // generic per-lane top-K select
+  int32_t select_lds_cap = 0;
+  bool select_generic = false;
   // sizes
   int32_t N = 0, D = 0, J = 0, U = 0;
   int32_t cap_N = 0, cap_U = 0, cap_J = 0, cap_rows = 0, cap_props = 0, cap_K = 0;
@@ -117,7 +126,7 @@ struct kp_ctx {
   std::string last_error;
 };
 
-// Kernel launchers (kp_kernels.hip).
+// Kernel launchers (kp_score.hip, kp_pass.hip).
 namespace kp {
 int launch_prep_nodes(kp_ctx *c, int32_t S, int most_allocated, const int32_t *w);
 int launch_score(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit,
@@ -129,7 +138,6 @@ int launch_open_init(kp_ctx *c, int32_t A, int32_t K);
 int launch_csr_build(kp_ctx *c, int32_t A, int32_t K);
 int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass);
 int launch_accept(kp_ctx *c, const ScoreParams &sp, int32_t pass, int32_t A);
-int launch_gang_commit(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass);
 int launch_active(kp_ctx *c, int32_t lo, int32_t hi, int32_t *A_host);
 int launch_reset_units(kp_ctx *c);
 int launch_finalize(kp_ctx *c);

@@ -4,19 +4,24 @@
 // After the candidate phase every active slot a has K candidate nodes
 // cand[a*K + c]. One radix sort per ROUND builds the node -> (slot,
 // candidate) inverse index in slot order (= unit rank order): entry e of the
-// sorted order belongs to node key[e]; inv[a*K + c] = e. A pass then needs no
-// sort and no host round trip:
+// sorted order belongs to node key[e]; inv[a*K + c] = e. A pass is then two
+// launches with no sort and no host round trip:
 //   plan   : a G-lane group per open slot (lane c = candidate c) plans the
 //            unit's members against the current usage and writes a
 //            pass-tagged bid (pass << 8 | members) straight into bid[inv[..]]
-//            plus a per-64-entry window flag;
-//   accept : one wave per node visits only its flagged windows, runs an exact
-//            parallel first-fit in rank order, commits units whose members
-//            all sit on this node (the wave owns the node: plain stores), and
-//            records ok[e] for multi-node gangs;
-//   gang   : all-or-nothing commit of multi-node gangs (int64 atomics).
+//            plus a per-64-entry window flag; a gang spread over several
+//            nodes also records its parts (node, members, offset, score);
+//   accept : one wave per node visits only its flagged windows and runs an
+//            exact parallel first-fit in rank order. A unit whose members all
+//            sit on this node is committed on the spot (the wave owns the
+//            node); a part of a multi-node gang bumps the gang's arrival
+//            counter, and the wave that accepts its LAST part commits the
+//            whole gang (all-or-nothing: a rejected part never arrives).
+// Every `used` update inside accept is an int64 atomic add, so the order in
+// which waves finish cannot change the result.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 
 #include <rocprim/rocprim.hpp>
@@ -31,14 +36,24 @@ using namespace dev;
 constexpr uint32_t kNoBid = 0xFFFFFFFFu;  // tag that matches no pass
 
 // ---- inverse index (once per round) --------------------------------------------
-__global__ void k_csr_keys(int32_t A, int32_t K, int32_t N, const int32_t *__restrict__ cand,
-                           uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+// Also re-initialises the round's pass state (bids, window flags, node
+// segments, pass flags) so no memset launch is needed.
+__global__ void k_csr_keys(int32_t A, int32_t K, int32_t N, int64_t nwin,
+                           const int32_t *__restrict__ cand, uint32_t *__restrict__ keys,
+                           uint32_t *__restrict__ vals, uint32_t *__restrict__ bid,
+                           int32_t *__restrict__ win, int32_t *__restrict__ seg_start,
+                           int32_t *__restrict__ pass_flag) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (int64_t)A * K) return;
-  const int32_t n = cand[t];
-  const int32_t a = (int32_t)(t / K), c = (int32_t)(t % K);
-  keys[t] = n >= 0 ? (uint32_t)n : (uint32_t)N;  // invalid entries sort after every node
-  vals[t] = ((uint32_t)a << 5) | (uint32_t)c;     // K <= 32
+  if (t < (int64_t)A * K) {
+    const int32_t n = cand[t];
+    const int32_t a = (int32_t)(t / K), c = (int32_t)(t % K);
+    keys[t] = n >= 0 ? (uint32_t)n : (uint32_t)N;  // invalid entries sort after every node
+    vals[t] = ((uint32_t)a << 5) | (uint32_t)c;     // K <= 32
+    bid[t] = kNoBid;
+  }
+  if (t < N) seg_start[t] = -1;
+  if (t < nwin) win[t] = -1;
+  if (t < 64) pass_flag[t] = 0;
 }
 
 __global__ void k_csr_finish(int32_t P, int32_t N, int32_t K, int32_t D, int32_t U,
@@ -72,7 +87,8 @@ __global__ void k_csr_finish(int32_t P, int32_t N, int32_t K, int32_t D, int32_t
 // G lanes per slot (G >= K), 64/G slots per wave. Members are planned one at a
 // time: each lane scores its candidate with the members it already holds,
 // subtracts the spread penalty of its topo domain, and the group takes the
-// (max value, lowest lane).
+// (max value, lowest lane). All first-level loads (slot state, unit, candidate,
+// entry index) are issued together, before the open test.
 template <int D, int G>
 __global__ __launch_bounds__(256) void k_plan(ScoreParams sp, int32_t A, int32_t U, int32_t pass,
                                               const int32_t *__restrict__ act,
@@ -90,7 +106,10 @@ __global__ __launch_bounds__(256) void k_plan(ScoreParams sp, int32_t A, int32_t
                                               uint32_t *__restrict__ bid,
                                               int32_t *__restrict__ win,
                                               int32_t *__restrict__ s0_out,
-                                              int32_t *__restrict__ pass_flag) {
+                                              int32_t *__restrict__ pass_flag,
+                                              int4 *__restrict__ gpart,
+                                              int32_t *__restrict__ nparts,
+                                              int32_t *__restrict__ arrive) {
   constexpr int SPW = 64 / G;  // slots per wave
   constexpr uint64_t GMASK = G == 64 ? ~0ull : ((1ull << G) - 1);
   const int lane = threadIdx.x & 63;
@@ -99,25 +118,27 @@ __global__ __launch_bounds__(256) void k_plan(ScoreParams sp, int32_t A, int32_t
   const int wave_global = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int a = wave_global * SPW + lane / G;
   const int K = sp.n_cand, N = sp.N;
-  const bool slot_ok = a < A && open[a];
+  const bool in = a < A;
+  const int aa = in ? a : 0;  // A > 0: slot 0 exists
+  const uint8_t op = open[aa];
+  const int32_t u0 = act[aa];
+  const int32_t node = gl < K ? cand[(int64_t)aa * K + gl] : -1;
+  const int32_t e_inv = gl < K ? inv[(int64_t)aa * K + gl] : 0;  // valid iff node >= 0
+  const bool slot_ok = in && op;
   if (__ballot(slot_ok) == 0) return;
-  int32_t u = 0, sz = 0;
+  const int32_t u = slot_ok ? u0 : 0;
+  const int32_t sz = slot_ok ? size[u] : 0;
   int64_t qq[D];
-  if (slot_ok) {
-    u = act[a];
-    sz = size[u];
-  }
 #pragma unroll
   for (int d = 0; d < D; ++d) qq[d] = slot_ok ? q[(int64_t)d * U + u] : 0;
-  const int32_t node = (slot_ok && gl < K) ? cand[(int64_t)a * K + gl] : -1;
-  const bool valid = node >= 0;
+  const bool valid = slot_ok && node >= 0;
   const int nn = valid ? node : 0;
-  int64_t c_[D], u0[D];
+  int64_t c_[D], u0_[D];
   uint64_t r_[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
     c_[d] = cap[(int64_t)d * N + nn];
-    u0[d] = used[(int64_t)d * N + nn];
+    u0_[d] = used[(int64_t)d * N + nn];
     r_[d] = R[(int64_t)d * N + nn];
   }
   const int64_t b = base[nn];
@@ -131,7 +152,7 @@ __global__ __launch_bounds__(256) void k_plan(ScoreParams sp, int32_t A, int32_t
     const bool live = !fail && m < sz;  // group-uniform
     int64_t uu[D];
 #pragma unroll
-    for (int d = 0; d < D; ++d) uu[d] = u0[d] + (int64_t)planned * qq[d];
+    for (int d = 0; d < D; ++d) uu[d] = u0_[d] + (int64_t)planned * qq[d];
     const int64_t s = (live && valid) ? score_at<D>(sp, qq, c_, uu, r_, b) : -1;
     if (m == 0) s0 = (int32_t)s;
     const bool feas = s >= 0;
@@ -147,6 +168,17 @@ __global__ __launch_bounds__(256) void k_plan(ScoreParams sp, int32_t A, int32_t
       dom += (valid && tp == wtp) ? 1 : 0;
     }
   }
+  // group-uniform from here on (slot_ok and fail are per group)
+  const bool prop = slot_ok && !fail && gl < K && planned > 0;
+  const uint64_t pm = (__ballot(prop) >> gbase) & GMASK;
+  const int np = __popcll(pm);
+  // member offset of this part = members of the earlier candidates
+  int32_t inc = planned;
+#pragma unroll
+  for (int d = 1; d < G; d <<= 1) {
+    const int32_t o = __shfl_up(inc, d, G);
+    if (gl >= d) inc += o;
+  }
   if (!slot_ok) return;
   if (fail) {
     if (gl == 0) {
@@ -155,13 +187,22 @@ __global__ __launch_bounds__(256) void k_plan(ScoreParams sp, int32_t A, int32_t
     }
     return;
   }
-  if (gl < K && planned > 0) {
-    const int32_t e = inv[(int64_t)a * K + gl];
-    bid[e] = ((uint32_t)pass << 8) | (uint32_t)planned;
-    s0_out[e] = s0;
-    win[e >> 6] = pass;
+  if (prop) {
+    bid[e_inv] = ((uint32_t)pass << 8) | (uint32_t)planned;
+    s0_out[e_inv] = s0;
+    win[e_inv >> 6] = pass;
+    if (np > 1) {
+      const int idx = __popcll(pm & ((1ull << gl) - 1));
+      gpart[(int64_t)a * K + idx] = make_int4(node, planned, inc - planned, s0);
+    }
   }
-  if (gl == 0) pass_flag[pass] = 1;
+  if (gl == 0) {
+    pass_flag[pass] = 1;
+    if (np > 1) {
+      nparts[a] = np;
+      arrive[a] = 0;
+    }
+  }
 }
 
 // ---- accept ----------------------------------------------------------------------
@@ -169,10 +210,8 @@ __global__ __launch_bounds__(256) void k_plan(ScoreParams sp, int32_t A, int32_t
 // order). Exact parallel first-fit per window: lanes that no longer fit alone are
 // rejected; among the rest the longest prefix whose running sum fits is accepted
 // and the first lane that breaks it is rejected (it cannot fit the reduced
-// remainder); repeat on what is left. A unit whose members all bid here (count ==
-// size) is committed on the spot; for multi-node gangs ok[e] = pass + 1 marks an
-// accepted part for k_gang_commit. The operands of the next flagged window are
-// loaded before the current one is decided (one HBM latency per window, hidden).
+// remainder); repeat on what is left. The operands of the next flagged windows
+// are loaded before the current one is decided (one HBM latency per batch).
 template <int D>
 struct Win {
   int32_t e, m, unit, size, lead, slot, s0;
@@ -206,16 +245,48 @@ __device__ __forceinline__ void load_win(Win<D> &w, int wi, int lane, int32_t e0
   for (int d = 0; d < D; ++d) w.need[d] = w.m > 0 ? (int64_t)w.m * w.need[d] : 0;
 }
 
+struct AcceptOut {
+  int32_t N, U, K;
+  const int4 *gpart;
+  const int32_t *nparts;
+  int32_t *arrive;
+  const int64_t *q;
+  int64_t *used;
+  uint8_t *open;
+  int32_t *status, *job_node, *job_score;
+};
+
+// all-or-nothing commit of a multi-node gang by the wave that accepted its
+// last part: every part's members go to the part's node, usage is added with
+// int64 atomics (other node waves may be folding into the same words)
+template <int D>
+__device__ __forceinline__ void commit_gang(const AcceptOut &o, int32_t slot, int32_t unit,
+                                         int32_t lead, int32_t np) {
+  int64_t qq[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) qq[d] = o.q[(int64_t)d * o.U + unit];
+  for (int i = 0; i < np; ++i) {
+    const int4 g = o.gpart[(int64_t)slot * o.K + i];
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      if (qq[d] != 0)
+        atomicAdd(reinterpret_cast<unsigned long long *>(&o.used[(int64_t)d * o.N + g.x]),
+                  (unsigned long long)((int64_t)g.y * qq[d]));
+    for (int m = 0; m < g.y; ++m) {
+      o.job_node[lead + g.z + m] = g.x;
+      o.job_score[lead + g.z + m] = g.w;
+    }
+  }
+  o.status[unit] = kPlaced;
+  o.open[slot] = 0;
+}
+
 // Exact parallel first-fit of one 64-entry window against the node's
 // remaining capacity `rem` (wave-uniform), in lane (= rank) order.
 template <int D>
 __device__ __forceinline__ void decide_window(const Win<D> &wc, int64_t (&rem)[D],
                                               int64_t (&add)[D], int lane, int node,
-                                              int32_t pass, uint8_t *__restrict__ ok,
-                                              uint8_t *__restrict__ open,
-                                              int32_t *__restrict__ status,
-                                              int32_t *__restrict__ job_node,
-                                              int32_t *__restrict__ job_score) {
+                                              const AcceptOut &o) {
   bool undecided = wc.m > 0, accepted = false;
   while (true) {
     bool fa = undecided;
@@ -248,15 +319,16 @@ __device__ __forceinline__ void decide_window(const Win<D> &wc, int64_t (&rem)[D
   if (wc.m > 0 && accepted) {
     if (wc.m == wc.size) {  // the whole unit bid on this node: commit now
       for (int i = 0; i < wc.m; ++i) {
-        job_node[wc.lead + i] = node;
-        job_score[wc.lead + i] = wc.s0;
+        o.job_node[wc.lead + i] = node;
+        o.job_score[wc.lead + i] = wc.s0;
       }
-      status[wc.unit] = kPlaced;
-      open[wc.slot] = 0;
+      o.status[wc.unit] = kPlaced;
+      o.open[wc.slot] = 0;
 #pragma unroll
       for (int d = 0; d < D; ++d) add[d] += wc.need[d];
-    } else {
-      ok[wc.e] = (uint8_t)(pass + 1);
+    } else {  // one part of a multi-node gang
+      const int32_t np = o.nparts[wc.slot];
+      if (atomicAdd(&o.arrive[wc.slot], 1) + 1 == np) commit_gang<D>(o, wc.slot, wc.unit, wc.lead, np);
     }
   }
 }
@@ -274,26 +346,21 @@ __global__ __launch_bounds__(256) void k_accept(ScoreParams sp, int32_t pass, in
                                                 const int32_t *__restrict__ ent_lead,
                                                 const int32_t *__restrict__ ent_slot,
                                                 const int64_t *__restrict__ cap,
-                                                int64_t *__restrict__ used,
-                                                uint8_t *__restrict__ ok,
-                                                uint8_t *__restrict__ open,
-                                                int32_t *__restrict__ status,
-                                                int32_t *__restrict__ job_node,
-                                                int32_t *__restrict__ job_score) {
+                                                AcceptOut o) {
   const int lane = threadIdx.x & 63;
   const int node = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int N = sp.N;
   if (node >= N) return;
   const int32_t e0 = seg_start[node];
-  if (e0 < 0) return;
   const int32_t e1 = seg_end[node];
-  const int32_t w0 = e0 >> 6, w1 = (e1 - 1) >> 6;
   int64_t rem[D], add[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    rem[d] = cap[(int64_t)d * N + node] - used[(int64_t)d * N + node];
+    rem[d] = cap[(int64_t)d * N + node] - o.used[(int64_t)d * N + node];
     add[d] = 0;
   }
+  if (e0 < 0) return;
+  const int32_t w0 = e0 >> 6, w1 = (e1 - 1) >> 6;
   constexpr int BATCH = 4;  // flagged windows whose operands are loaded together
   for (int wb = w0; wb <= w1; wb += 64) {
     uint64_t flagged = __ballot(wb + lane <= w1 && win[wb + lane] == pass);
@@ -311,89 +378,18 @@ __global__ __launch_bounds__(256) void k_accept(ScoreParams sp, int32_t pass, in
                     ent_lead, ent_slot, s0);
 #pragma unroll
       for (int t = 0; t < BATCH; ++t) {
-        Win<D> &wc = wv[t];
         if (wl[t] < 0) break;
-        decide_window<D>(wc, rem, add, lane, node, pass, ok, open, status, job_node, job_score);
+        decide_window<D>(wv[t], rem, add, lane, node, o);
       }
     }
   }
-  // this wave owns the node: fold the committed single-node units into `used`
+  // fold the single-node units committed by this wave into `used`
 #pragma unroll
   for (int d = 0; d < D; ++d) {
     const int64_t tot = wave_incl_scan_i64(add[d]);
-    if (lane == 63 && tot != 0) used[(int64_t)d * N + node] += tot;
-  }
-}
-
-// ---- multi-node gang commit --------------------------------------------------------
-// A G-lane group per slot, lane c = candidate c: all-or-nothing over the parts
-// accepted this pass; members map to nodes in candidate order.
-template <int G>
-__global__ __launch_bounds__(256) void k_gang_commit(int32_t A, int32_t K, int32_t D, int32_t N,
-                                                     int32_t U, int32_t pass,
-                                                     const int32_t *__restrict__ act,
-                                                     const int32_t *__restrict__ cand,
-                                                     const int32_t *__restrict__ inv,
-                                                     const uint32_t *__restrict__ bid,
-                                                     const int32_t *__restrict__ s0,
-                                                     const uint8_t *__restrict__ ok,
-                                                     const int64_t *__restrict__ q,
-                                                     const int32_t *__restrict__ size,
-                                                     const int32_t *__restrict__ leader,
-                                                     uint8_t *__restrict__ open,
-                                                     int32_t *__restrict__ status,
-                                                     int64_t *__restrict__ used,
-                                                     int32_t *__restrict__ job_node,
-                                                     int32_t *__restrict__ job_score) {
-  constexpr int SPW = 64 / G;
-  constexpr uint64_t GMASK = G == 64 ? ~0ull : ((1ull << G) - 1);
-  const int lane = threadIdx.x & 63;
-  const int gl = lane & (G - 1), gbase = lane & ~(G - 1);
-  const int a = (blockIdx.x * 4 + (threadIdx.x >> 6)) * SPW + lane / G;
-  bool live = a < A && open[a];
-  int32_t u = 0, sz = 1;
-  if (live) {
-    u = act[a];
-    sz = size[u];
-    live = sz > 1;  // singletons and single-node gangs are decided in k_accept
-  }
-  if (__ballot(live) == 0) return;
-  int32_t m = 0, e = 0, node = -1;
-  bool part_ok = true;
-  if (live && gl < K) {
-    node = cand[(int64_t)a * K + gl];
-    if (node >= 0) {
-      e = inv[(int64_t)a * K + gl];
-      const uint32_t t = bid[e];
-      if ((t >> 8) == (uint32_t)pass) {
-        m = (int32_t)(t & 0xFFu);
-        part_ok = ok[e] == (uint8_t)(pass + 1);
-      }
-    }
-  }
-  const uint64_t has = (__ballot(m > 0) >> gbase) & GMASK;
-  const uint64_t bad = (__ballot(m > 0 && !part_ok) >> gbase) & GMASK;
-  const uint64_t whole = (__ballot(m > 0 && m == sz) >> gbase) & GMASK;
-  if (!live || has == 0 || bad != 0 || whole != 0) return;
-  // member offset = members of the earlier candidates of this slot
-  int32_t off = 0;
-  for (int c = 0; c < G; ++c) {
-    const int32_t mc = __shfl(m, gbase + c, 64);
-    if (c < gl) off += mc;
-  }
-  if (m > 0) {
-    for (int d = 0; d < D; ++d)
-      atomicAdd(reinterpret_cast<unsigned long long *>(&used[(int64_t)d * N + node]),
-                (unsigned long long)((int64_t)m * q[(int64_t)d * U + u]));
-    const int32_t j0 = leader[u] + off, sc = s0[e];
-    for (int i = 0; i < m; ++i) {
-      job_node[j0 + i] = node;
-      job_score[j0 + i] = sc;
-    }
-  }
-  if (gl == 0) {
-    status[u] = kPlaced;
-    open[a] = 0;
+    if (lane == 63 && tot != 0)
+      atomicAdd(reinterpret_cast<unsigned long long *>(&o.used[(int64_t)d * N + node]),
+                (unsigned long long)tot);
   }
 }
 
@@ -405,13 +401,15 @@ struct PlanL {
       hipLaunchKernelGGL((k_plan<D, G>), dim3(blocks(A, 4 * (64 / G))), dim3(256), 0, c->stream,
                          sp, A, c->U, pass, c->d.act, c->d.cand, c->d.inv, c->d.open,
                          c->d.status, c->d.cap, c->d.used, c->d.R, c->d.base, c->d.topo, c->d.q,
-                         c->d.size, c->d.bid, c->d.win, c->d.s0, c->d.pass_flag);
+                         c->d.size, c->d.bid, c->d.win, c->d.s0, c->d.pass_flag, c->d.gpart,
+                         c->d.nparts, c->d.arrive);
     } else {
       constexpr int G = 32;
       hipLaunchKernelGGL((k_plan<D, G>), dim3(blocks(A, 4 * (64 / G))), dim3(256), 0, c->stream,
                          sp, A, c->U, pass, c->d.act, c->d.cand, c->d.inv, c->d.open,
                          c->d.status, c->d.cap, c->d.used, c->d.R, c->d.base, c->d.topo, c->d.q,
-                         c->d.size, c->d.bid, c->d.win, c->d.s0, c->d.pass_flag);
+                         c->d.size, c->d.bid, c->d.win, c->d.s0, c->d.pass_flag, c->d.gpart,
+                         c->d.nparts, c->d.arrive);
     }
     KP_HIP(hipGetLastError());
     return KP_OK;
@@ -421,11 +419,22 @@ struct PlanL {
 template <int D>
 struct AcceptL {
   static int run(kp_ctx *c, const ScoreParams &sp, int32_t pass, int64_t P) {
+    AcceptOut o;
+    o.N = c->N;
+    o.U = c->U;
+    o.K = sp.n_cand;
+    o.gpart = c->d.gpart;
+    o.nparts = c->d.nparts;
+    o.arrive = c->d.arrive;
+    o.q = c->d.q;
+    o.used = c->d.used;
+    o.open = c->d.open;
+    o.status = c->d.status;
+    o.job_node = c->d.job_node;
+    o.job_score = c->d.job_score;
     hipLaunchKernelGGL((k_accept<D>), dim3(blocks(c->N, 4)), dim3(256), 0, c->stream, sp, pass,
                        P, c->d.seg_start, c->d.seg_end, c->d.bid, c->d.win, c->d.s0, c->d.ent_q,
-                       c->d.ent_unit, c->d.ent_size, c->d.ent_lead, c->d.ent_slot, c->d.cap,
-                       c->d.used, c->d.ok, c->d.open, c->d.status, c->d.job_node,
-                       c->d.job_score);
+                       c->d.ent_unit, c->d.ent_size, c->d.ent_lead, c->d.ent_slot, c->d.cap, o);
     KP_HIP(hipGetLastError());
     return KP_OK;
   }
@@ -446,19 +455,18 @@ size_t rocprim_temp_bytes(int32_t max_items) {
 // node -> bidder inverse index of this round's candidates (one sort per round)
 int launch_csr_build(kp_ctx *c, int32_t A, int32_t K) {
   const int64_t P = (int64_t)A * K;
-  KP_HIP(hipMemsetAsync(c->d.seg_start, 0xFF, sizeof(int32_t) * c->N, c->stream));
-  if (P == 0) return KP_OK;
-  KP_HIP(hipMemsetAsync(c->d.bid, 0xFF, sizeof(uint32_t) * P, c->stream));
-  KP_HIP(hipMemsetAsync(c->d.win, 0xFF, sizeof(int32_t) * ((P + 63) / 64 + 64), c->stream));
-  hipLaunchKernelGGL(k_csr_keys, dim3(blocks(P, 256)), dim3(256), 0, c->stream, A, K, c->N,
-                     c->d.cand, c->d.csr_kin, c->d.csr_vin);
+  const int64_t nwin = (P + 63) / 64 + 64;
+  const int64_t n = std::max<int64_t>(std::max<int64_t>(P, c->N), std::max<int64_t>(nwin, 64));
+  hipLaunchKernelGGL(k_csr_keys, dim3(blocks(n, 256)), dim3(256), 0, c->stream, A, K, c->N, nwin,
+                     c->d.cand, c->d.csr_kin, c->d.csr_vin, c->d.bid, c->d.win, c->d.seg_start,
+                     c->d.pass_flag);
   KP_HIP(hipGetLastError());
+  if (P == 0) return KP_OK;
   unsigned bits = 1;
   while ((1ll << bits) <= c->N) ++bits;  // key N (invalid) must fit too
   size_t tb = c->d.temp_bytes;
   KP_HIP(rocprim::radix_sort_pairs(c->d.temp, tb, c->d.csr_kin, c->d.csr_keys, c->d.csr_vin,
                                    c->d.csr_vals, (size_t)P, 0u, bits, c->stream));
-  KP_HIP(hipMemsetAsync(c->d.ok, 0, P, c->stream));
   hipLaunchKernelGGL(k_csr_finish, dim3(blocks(P, 256)), dim3(256), 0, c->stream, (int32_t)P,
                      c->N, K, c->D, c->U, c->d.csr_keys, c->d.csr_vals, c->d.act, c->d.q,
                      c->d.size, c->d.leader, c->d.seg_start, c->d.seg_end, c->d.inv,
@@ -475,25 +483,6 @@ int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass) {
 int launch_accept(kp_ctx *c, const ScoreParams &sp, int32_t pass, int32_t A) {
   if (c->N <= 0 || A <= 0) return KP_OK;
   return dispatch_D<AcceptL>(c->D, c, sp, pass, (int64_t)A * sp.n_cand);
-}
-
-int launch_gang_commit(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass) {
-  if (A <= 0) return KP_OK;
-  if (sp.n_cand <= 16) {
-    constexpr int G = 16;
-    hipLaunchKernelGGL(k_gang_commit<G>, dim3(blocks(A, 4 * (64 / G))), dim3(256), 0, c->stream,
-                       A, sp.n_cand, c->D, c->N, c->U, pass, c->d.act, c->d.cand, c->d.inv,
-                       c->d.bid, c->d.s0, c->d.ok, c->d.q, c->d.size, c->d.leader, c->d.open,
-                       c->d.status, c->d.used, c->d.job_node, c->d.job_score);
-  } else {
-    constexpr int G = 32;
-    hipLaunchKernelGGL(k_gang_commit<G>, dim3(blocks(A, 4 * (64 / G))), dim3(256), 0, c->stream,
-                       A, sp.n_cand, c->D, c->N, c->U, pass, c->d.act, c->d.cand, c->d.inv,
-                       c->d.bid, c->d.s0, c->d.ok, c->d.q, c->d.size, c->d.leader, c->d.open,
-                       c->d.status, c->d.used, c->d.job_node, c->d.job_score);
-  }
-  KP_HIP(hipGetLastError());
-  return KP_OK;
 }
 
 }  // namespace kp

@@ -8,6 +8,7 @@
 // argmax and prefix sums.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 
 #include <rocprim/rocprim.hpp>
@@ -37,11 +38,11 @@ __global__ void k_prep_nodes(const int64_t *__restrict__ cap, uint64_t *__restri
 }
 
 // ---------------------------------------------------------------------------
-// filter + score (materialised). One 256-thread workgroup owns a tile of
-// 4 waves x 64 lanes x NPL nodes; the tile's cap/used/R stay in VGPRs while
-// the workgroup streams `rows_per_block` job rows past it: per row the
-// request is wave-uniform (scalar loads), each lane stores NPL int32 scores
-// (coalesced 256-B wave stores) and the wave ballots the feasibility bits
+// filter + score (materialised), 64-bit path (some cap or request >= 2^32).
+// One 256-thread workgroup owns a tile of 4 waves x 64 lanes x NPL nodes; the
+// tile's cap/used/R stay in VGPRs while the workgroup streams
+// `rows_per_block` job rows past it: per row the request is wave-uniform,
+// each lane stores NPL int32 scores and the wave ballots the feasibility bits
 // straight into the row's mask words.
 // Row stride of score/mask = Ns = round_up(N, 64); padding is infeasible.
 // ---------------------------------------------------------------------------
@@ -104,7 +105,34 @@ __global__ __launch_bounds__(256) void k_score(ScoreParams sp,
 // util = ((u * R) >> 32) with R = Rh*2^32 + Rl (Rh <= S) is
 // mulhi(u, Rl) + u*Rh exactly, since u*Rh*2^32 is a multiple of 2^32.
 // Halves the VALU work per pair so the kernel stays on the HBM store roof.
-template <int D, int NPL>
+//
+// Layout: lane l of wave w owns the 4 CONSECUTIVE nodes tile0 + 4l .. +3, so a
+// row's scores leave as one 16-B store per lane (1 KiB per wave instruction,
+// whole 128-B lines). The 4 per-k ballots are bit-interleaved into the row's
+// 4 mask words (word i bit 4j+k = ballot_k bit 16i+j). The requests of the
+// workgroup's rows are gathered into LDS once, so the rows_unit -> q load
+// chain is paid per workgroup, not per row.
+__device__ __forceinline__ uint64_t spread4_16(uint64_t x) {
+  // bit j of a 16-bit value -> bit 4j
+  x &= 0xFFFFull;
+  x = (x | (x << 24)) & 0x000000FF000000FFull;
+  x = (x | (x << 12)) & 0x000F000F000F000Full;
+  x = (x | (x << 6)) & 0x0303030303030303ull;
+  x = (x | (x << 3)) & 0x1111111111111111ull;
+  return x;
+}
+
+constexpr int kScoreMaxRows = 32;  // rows per workgroup (LDS request stage)
+
+// v_mul_u32_u24 as written: the compiler otherwise fuses the 24-bit product
+// with the mulhi sum into a (much slower) v_mad_u64_u32
+__device__ __forceinline__ uint32_t mul_u24(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+template <int D>
 __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
                                                  const int64_t *__restrict__ cap,
                                                  const int64_t *__restrict__ used,
@@ -115,15 +143,24 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
                                                  int32_t rows, int32_t rows_per_block,
                                                  int32_t *__restrict__ score,
                                                  uint64_t *__restrict__ mask, int32_t Ns) {
+  constexpr int NPL = 4;
+  __shared__ uint32_t sq[kScoreMaxRows][D];
   const int N = sp.N;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int tile0 = blockIdx.x * (256 * NPL) + wave * (64 * NPL);
+  const int tile0 = blockIdx.x * 1024 + wave * 256;
+  const int nb = tile0 + lane * NPL;  // first of this lane's 4 nodes
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  if ((int)threadIdx.x < (r1 - r0) * D) {
+    const int rr = threadIdx.x / D, d = threadIdx.x % D;
+    sq[rr][d] = (uint32_t)q[(int64_t)d * qstride + rows_unit[r0 + rr]];
+  }
   uint32_t f_[NPL][D], u_[NPL][D], rl_[NPL][D], rh_[NPL][D];
   int32_t b_[NPL];
   bool v_[NPL];
 #pragma unroll
   for (int k = 0; k < NPL; ++k) {
-    const int n = tile0 + k * 64 + lane;
+    const int n = nb + k;
     v_[k] = n < N;
     const int nn = v_[k] ? n : 0;
 #pragma unroll
@@ -137,44 +174,202 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
     }
     b_[k] = (int32_t)base[nn];
   }
+  __syncthreads();
+  if (tile0 >= Ns) return;  // wave-uniform, after the only barrier
   const int words = Ns >> 6;
-  const int r0 = blockIdx.y * rows_per_block;
-  const int r1 = min(rows, r0 + rows_per_block);
-  if (tile0 >= Ns) return;
+  const bool store_ok = nb < Ns;  // Ns % 64 == 0: then all 4 nodes are in the row
   for (int r = r0; r < r1; ++r) {
-    const int32_t unit = rows_unit[r];
     uint32_t qq[D];
 #pragma unroll
-    for (int d = 0; d < D; ++d) qq[d] = (uint32_t)q[(int64_t)d * qstride + unit];
-    int32_t *srow = score + (int64_t)r * Ns;
+    for (int d = 0; d < D; ++d) qq[d] = sq[r - r0][d];
+    int32_t sv[NPL];
+    uint64_t bal[NPL];
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
-      const int n = tile0 + k * 64 + lane;
       bool fits = v_[k];
       int32_t acc = 0, fit_bonus = 0;
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         fits &= qq[d] <= f_[k][d];
         const uint32_t uu = u_[k][d] + qq[d];
-        const uint32_t util = __umulhi(uu, rl_[k][d]) + uu * rh_[k][d];
-        acc += sp.w[d] * (int32_t)util;
+        // 24-bit multiplies (full rate) are exact wherever the pair fits:
+        // rh > 0 only if cap <= S <= 1024, and then uu <= cap; w <= 65535 and
+        // util <= S. Only mulhi stays a 32-bit (quarter-rate) multiply.
+        const uint32_t util = __umulhi(uu, rl_[k][d]) + mul_u24(uu, rh_[k][d]);
+        acc += (int32_t)__umul24((uint32_t)sp.w[d], util);
         if (d == sp.gpu_dim && qq[d] > 0 && f_[k][d] == qq[d]) fit_bonus = sp.w_gpu_fit;
       }
       const int32_t s = (sp.most_allocated ? acc : b_[k] - acc) + fit_bonus;
-      if (score && n < Ns) srow[n] = fits ? s : KP_SCORE_INFEASIBLE;
-      const uint64_t bits = __ballot(fits);
-      if (mask && lane == 0 && (tile0 + k * 64) < Ns)
-        mask[(int64_t)r * words + ((tile0 + k * 64) >> 6)] = bits;
+      sv[k] = fits ? s : KP_SCORE_INFEASIBLE;
+      bal[k] = __ballot(fits);
+    }
+    if (score && store_ok)
+      *reinterpret_cast<int4 *>(score + (int64_t)r * Ns + nb) =
+          make_int4(sv[0], sv[1], sv[2], sv[3]);
+    if (mask && lane < 4 && tile0 + 64 * lane < Ns) {
+      const int sh = 16 * lane;
+      const uint64_t wd = spread4_16(bal[0] >> sh) | (spread4_16(bal[1] >> sh) << 1) |
+                          (spread4_16(bal[2] >> sh) << 2) | (spread4_16(bal[3] >> sh) << 3);
+      mask[(int64_t)r * words + (tile0 >> 6) + lane] = wd;
     }
   }
 }
 
 // ---------------------------------------------------------------------------
-// top-K select: one wave per score-matrix row. Each lane keeps its own
-// descending top-KC list of packed keys (valid bit | score | ~tie key) over a
-// strided slice of the row (16-B loads: 4 nodes per lane per step), then the
-// wave merges the 64 lists KC times with a butterfly max. Exact: every global
-// top-K entry is in its lane's top-K.
+// Candidate keys: (valid bit | score | ~tie key), unique per node because the
+// tie key is a bijection of the node index. Larger = better.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t pack_key(int32_t s, uint32_t tk) {
+  return (1ull << 63) | ((uint64_t)(uint32_t)s << 32) | (uint64_t)(~tk);
+}
+__device__ __forceinline__ int32_t key_node(uint64_t key, uint32_t sl, uint32_t inv) {
+  const uint32_t tk = ~(uint32_t)key;
+  return (int32_t)((tk - sl) * inv);
+}
+__device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+
+// ---------------------------------------------------------------------------
+// top-K select, threshold form (rows of up to 65536 nodes). One workgroup of
+// BS threads per score row; the row is held in registers (V4 16-B loads per
+// thread, all issued before any is consumed).
+//  1. every thread's best key;
+//  2. each wave sorts its 64 thread-bests (bitonic network over lane
+//     shuffles); the K-th of them is a lower bound on the row's K-th key
+//     (K distinct nodes reach it), so T = their max over the waves is one too;
+//  3. keys >= T are appended to an LDS buffer (typically K..4K of them);
+//  4. rank counting in LDS gives each survivor its exact position; ranks < K
+//     are the candidates, best first.
+// If more than `lds_cap` keys survive, T is raised to the K-th largest
+// buffered key (again a valid bound: K distinct keys reach it; strictly larger
+// than T since the buffer holds > K distinct keys >= T) and step 3 repeats.
+// Exact for every input; bit-exact with oracle kpo_round_candidates.
+// ---------------------------------------------------------------------------
+constexpr int kSelLdsCap = 1024;
+
+template <int V4, int BS>
+__global__ __launch_bounds__(BS) void k_select_t(ScoreParams sp,
+                                                 const int32_t *__restrict__ score, int32_t Ns,
+                                                 const int32_t *__restrict__ rows_unit,
+                                                 const uint32_t *__restrict__ salt, int32_t rows,
+                                                 int32_t lds_cap, int32_t *__restrict__ cand) {
+  constexpr int NW = BS / 64;
+  __shared__ uint64_t buf[kSelLdsCap];
+  __shared__ uint64_t wth[NW];
+  __shared__ uint64_t raised;
+  __shared__ int cnt;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row = blockIdx.x;
+  if (row >= rows) return;  // block-uniform
+  const int K = sp.n_cand;
+  const int32_t unit = rows_unit[row];
+  const uint32_t sl = sp.tie_rotated ? salt[unit] : 0u;
+  const uint32_t mul = sp.tie_rotated ? kTieMul : 1u;
+  const uint32_t inv = sp.tie_rotated ? kTieMulInv : 1u;
+  const int4 *row4 = reinterpret_cast<const int4 *>(score + (int64_t)row * Ns);
+  const int n4 = Ns >> 2;
+  int4 v[V4];
+#pragma unroll
+  for (int t = 0; t < V4; ++t) {
+    const int i = tid + BS * t;
+    v[t] = i < n4 ? row4[i] : make_int4(-1, -1, -1, -1);
+  }
+  // tie keys advance by a constant per element: node 4*(tid + BS*t) + j has
+  // tk = tk0 + t*step + j*mul (mod 2^32), so no per-element multiply
+  const uint32_t tk0 = (uint32_t)(4 * tid) * mul + sl;
+  const uint32_t step = (uint32_t)(4 * BS) * mul;
+  const uint32_t m1 = mul, m2 = 2u * mul, m3 = 3u * mul;
+  // 1. thread best: max score, then the smallest tie key among its holders
+  int32_t smax = -1;
+#pragma unroll
+  for (int t = 0; t < V4; ++t) smax = max(smax, max(max(v[t].x, v[t].y), max(v[t].z, v[t].w)));
+  uint32_t tkmin = 0xFFFFFFFFu;
+#pragma unroll
+  for (int t = 0; t < V4; ++t) {
+    const uint32_t tk = tk0 + (uint32_t)t * step;
+    tkmin = min(tkmin, v[t].x == smax ? tk : 0xFFFFFFFFu);
+    tkmin = min(tkmin, v[t].y == smax ? tk + m1 : 0xFFFFFFFFu);
+    tkmin = min(tkmin, v[t].z == smax ? tk + m2 : 0xFFFFFFFFu);
+    tkmin = min(tkmin, v[t].w == smax ? tk + m3 : 0xFFFFFFFFu);
+  }
+  uint64_t x = smax >= 0 ? pack_key(smax, tkmin) : 0ull;
+  // bitonic sort of the wave's 64 thread-bests, descending across lanes
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const uint64_t o = shfl_xor_u64(x, j);
+      const bool take_max = ((lane & j) == 0) == ((lane & k) == 0);
+      x = take_max ? umax64(x, o) : umin64(x, o);
+    }
+  }
+  const uint64_t tw = (uint64_t)shfl_i64((int64_t)x, K - 1);
+  if (lane == 0) wth[wave] = tw;
+  if (tid == 0) cnt = 0;
+  __syncthreads();
+  uint64_t T = 1;  // every valid key has bit 63 set
+#pragma unroll
+  for (int w = 0; w < NW; ++w) T = umax64(T, wth[w]);
+  int C;
+  while (true) {
+    // key >= T  <=>  s >= 0 and (s > Ts or (s == Ts and tk <= Tk)); T == 1
+    // (no bound) maps to Ts = -1: every feasible entry
+    const int32_t Ts = T == 1 ? -1 : (int32_t)((T >> 32) & 0x7FFFFFFFu);
+    const uint32_t Tk = ~(uint32_t)T;
+    // branch-free test of every held entry -> one bit each; the (rare)
+    // survivors are then appended one at a time, re-reading their score
+    uint64_t hits = 0;
+#pragma unroll
+    for (int t = 0; t < V4; ++t) {
+      const int32_t sv[4] = {v[t].x, v[t].y, v[t].z, v[t].w};
+      const uint32_t tk = tk0 + (uint32_t)t * step;
+      const uint32_t tj[4] = {tk, tk + m1, tk + m2, tk + m3};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int32_t s = sv[j];
+        const bool h = (s > Ts) | ((s == Ts) & (tj[j] <= Tk));
+        hits |= (uint64_t)(h & (s >= 0)) << (4 * t + j);
+      }
+    }
+    while (hits) {
+      const int bpos = __ffsll((unsigned long long)hits) - 1;
+      hits &= hits - 1;
+      const int t = bpos >> 2, j = bpos & 3;
+      const int32_t s = score[(int64_t)row * Ns + 4 * (tid + BS * t) + j];
+      const uint32_t tk = tk0 + (uint32_t)t * step + (uint32_t)j * m1;
+      const int p = atomicAdd(&cnt, 1);
+      if (p < lds_cap) buf[p] = pack_key(s, tk);
+    }
+    __syncthreads();
+    C = cnt;
+    if (C <= lds_cap) break;  // block-uniform
+    // overflow: raise T to the K-th largest buffered key
+    for (int i = tid; i < lds_cap; i += BS) {
+      const uint64_t ki = buf[i];
+      int r = 0;
+      for (int jj = 0; jj < lds_cap; ++jj) r += buf[jj] > ki ? 1 : 0;
+      if (r == K - 1) raised = ki;
+    }
+    __syncthreads();
+    T = raised;
+    if (tid == 0) cnt = 0;
+    __syncthreads();
+  }
+  for (int i = tid; i < C; i += BS) {
+    const uint64_t ki = buf[i];
+    int r = 0;
+    for (int jj = 0; jj < C; ++jj) r += buf[jj] > ki ? 1 : 0;
+    if (r < K) cand[(int64_t)row * K + r] = key_node(ki, sl, inv);
+  }
+  if (tid >= C && tid < K) cand[(int64_t)row * K + tid] = -1;
+}
+
+// ---------------------------------------------------------------------------
+// top-K select, generic form (rows of any length): one 256-thread workgroup
+// per row. Each lane keeps its own descending top-KC list over a strided slice
+// of the row (16-B loads: 4 nodes per lane per step), then each wave merges
+// its 64 lists K times with a butterfly max and wave 0 merges the 4 wave
+// lists from LDS. Exact: every global top-K entry is in its lane's top-K.
 // ---------------------------------------------------------------------------
 template <int KC>
 __device__ __forceinline__ void topk_insert(uint64_t (&k)[KC], uint64_t x) {
@@ -189,18 +384,12 @@ __device__ __forceinline__ void topk_insert(uint64_t (&k)[KC], uint64_t x) {
   }
 }
 
-__device__ __forceinline__ uint64_t pack_key(int32_t s, uint32_t tk) {
-  return (1ull << 63) | ((uint64_t)(uint32_t)s << 32) | (uint64_t)(~tk);
-}
-
 template <int KC>
 __global__ __launch_bounds__(256) void k_select(ScoreParams sp,
                                                 const int32_t *__restrict__ score, int32_t Ns,
                                                 const int32_t *__restrict__ rows_unit,
                                                 const uint32_t *__restrict__ salt,
                                                 int32_t rows, int32_t *__restrict__ cand) {
-  // one 256-thread workgroup per row: 4 waves split the row, each wave merges
-  // its lanes' lists, wave 0 merges the 4 wave lists from LDS
   __shared__ uint64_t part[4][KC];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int row = blockIdx.x;
@@ -256,14 +445,7 @@ __global__ __launch_bounds__(256) void k_select(ScoreParams sp,
   const uint32_t inv = sp.tie_rotated ? kTieMulInv : 1u;
   for (int it = 0; it < K; ++it) {
     const uint64_t m = wave_max_u64(h0);
-    if (lane == 0) {
-      int32_t node = -1;
-      if (m != 0) {
-        const uint32_t tk = ~(uint32_t)m;
-        node = (int32_t)((tk - sl) * inv);
-      }
-      cand[(int64_t)row * K + it] = node;
-    }
+    if (lane == 0) cand[(int64_t)row * K + it] = m != 0 ? key_node(m, sl, inv) : -1;
     if (m != 0 && h0 == m) {
       h0 = h1;
       h1 = 0;
@@ -349,15 +531,18 @@ struct ScoreL {
   static int run(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
                  int32_t *score, uint64_t *mask, const int64_t *q, int32_t qstride) {
     const int Ns = (c->N + 63) & ~63;
-    const int rpb = 32;
     if (c->fits32) {
-      constexpr int NPL = D <= 4 ? 4 : 2;
-      dim3 grid(blocks(Ns, 256 * NPL), blocks(rows, rpb));
-      hipLaunchKernelGGL((k_score32<D, NPL>), grid, dim3(256), 0, c->stream, sp, c->d.cap,
-                         c->d.used, c->d.R, c->d.base, q, qstride, rows_unit, rows, rpb, score,
-                         mask, Ns);
+      // rows per workgroup: enough workgroups to cover the 256 CUs several
+      // times over, at most kScoreMaxRows (the LDS request stage)
+      const int tiles = blocks(Ns, 1024);
+      const int64_t want = ((int64_t)rows * tiles + 2047) / 2048;
+      const int rpb = (int)std::min<int64_t>(kScoreMaxRows, std::max<int64_t>(4, want));
+      dim3 grid(tiles, blocks(rows, rpb));
+      hipLaunchKernelGGL((k_score32<D>), grid, dim3(256), 0, c->stream, sp, c->d.cap, c->d.used,
+                         c->d.R, c->d.base, q, qstride, rows_unit, rows, rpb, score, mask, Ns);
     } else {
       constexpr int NPL = D <= 4 ? 2 : 1;
+      const int rpb = 32;
       dim3 grid(blocks(Ns, 256 * NPL), blocks(rows, rpb));
       hipLaunchKernelGGL((k_score<D, NPL>), grid, dim3(256), 0, c->stream, sp, c->d.cap,
                          c->d.used, c->d.R, c->d.base, q, qstride, rows_unit, rows, rpb, score,
@@ -393,16 +578,41 @@ int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, in
                   const int32_t *score, int32_t *cand) {
   if (rows <= 0) return KP_OK;
   const int Ns = (c->N + 63) & ~63;
-  dim3 grid(rows), blk(256);  // one workgroup per row
   const int K = sp.n_cand;
-  if (K <= 4)
-    hipLaunchKernelGGL(k_select<4>, grid, blk, 0, c->stream, sp, score, Ns, rows_unit, c->d.salt, rows, cand);
-  else if (K <= 8)
-    hipLaunchKernelGGL(k_select<8>, grid, blk, 0, c->stream, sp, score, Ns, rows_unit, c->d.salt, rows, cand);
-  else if (K <= 16)
-    hipLaunchKernelGGL(k_select<16>, grid, blk, 0, c->stream, sp, score, Ns, rows_unit, c->d.salt, rows, cand);
-  else
-    hipLaunchKernelGGL(k_select<32>, grid, blk, 0, c->stream, sp, score, Ns, rows_unit, c->d.salt, rows, cand);
+  const int lim = c->select_lds_cap > 0 ? std::min(c->select_lds_cap, kSelLdsCap) : kSelLdsCap;
+  const int cap = std::max(K + 1, lim);
+  const bool generic = c->select_generic || Ns > 4096 * 16;
+  dim3 grid(rows);
+#define KP_SEL_T(V4, BS)                                                                 \
+  hipLaunchKernelGGL((k_select_t<V4, BS>), grid, dim3(BS), 0, c->stream, sp, score, Ns,  \
+                     rows_unit, c->d.salt, rows, cap, cand)
+  if (generic) {
+    if (K <= 4)
+      hipLaunchKernelGGL(k_select<4>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
+                         c->d.salt, rows, cand);
+    else if (K <= 8)
+      hipLaunchKernelGGL(k_select<8>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
+                         c->d.salt, rows, cand);
+    else if (K <= 16)
+      hipLaunchKernelGGL(k_select<16>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
+                         c->d.salt, rows, cand);
+    else
+      hipLaunchKernelGGL(k_select<32>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
+                         c->d.salt, rows, cand);
+  } else if (Ns <= 1024 * 1) {
+    KP_SEL_T(1, 256);
+  } else if (Ns <= 1024 * 2) {
+    KP_SEL_T(2, 256);
+  } else if (Ns <= 1024 * 4) {
+    KP_SEL_T(4, 256);
+  } else if (Ns <= 1024 * 8) {
+    KP_SEL_T(8, 256);
+  } else if (Ns <= 1024 * 16) {
+    KP_SEL_T(16, 256);
+  } else {
+    KP_SEL_T(16, 1024);
+  }
+#undef KP_SEL_T
   KP_HIP(hipGetLastError());
   return KP_OK;
 }

@@ -134,6 +134,33 @@ def test_place_config3_small_parity(oracle, placer):
     _assert_same(g, o, "config3 20k")
 
 
+@pytest.mark.parametrize("knob,n_cand,tie", [
+    (("KP_SELECT_LDS_CAP", "33"), 16, 1),   # threshold select, threshold-raise path
+    (("KP_SELECT_LDS_CAP", "33"), 32, 0),
+    (("KP_SELECT_GENERIC", "1"), 16, 1),    # generic per-lane top-K select
+    (("KP_SELECT_GENERIC", "1"), 5, 0),
+])
+def test_select_paths_parity(oracle, monkeypatch, knob, n_cand, tie):
+    """Every top-K select form gives the oracle's candidates (checked through
+    the whole placement, which depends on every candidate list)."""
+    monkeypatch.setenv(*knob)
+    w = synth.config3(6_000, 600)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[3], n_cand=n_cand, tie_mode=tie)
+    with Placer(device=0) as pl:
+        g = pl.place(w, p)
+    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
+    _assert_same(g, o, f"{knob} K={n_cand}")
+
+
+def test_place_wide_rows_parity(oracle, placer):
+    """Rows above 16384 nodes take the 1024-thread select form."""
+    w = synth.config2(3_000, 20_000)
+    w.used = (w.cap * (np.arange(w.N) % 7) // 9).astype(np.int64)  # uneven usage
+    p = _abi.default_params(**synth.CONFIG_PARAMS[2])
+    g, o = _place_both(oracle, placer, w, p)
+    _assert_same(g, o, "wide rows")
+
+
 def test_place_config3_full_parity_and_properties(oracle, placer):
     """BASELINE config #3 at full size: bit-exact + size-independent checks."""
     w = synth.config3()
