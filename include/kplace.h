@@ -179,6 +179,38 @@ int kp_reset_nodes(kp_ctx *ctx);
 int kp_score(kp_ctx *ctx, const kp_params *p, int32_t job_lo, int32_t job_hi,
              int32_t *score, uint64_t *mask);
 
+/*
+ * Preemption candidates (BASELINE config #4).
+ *
+ * The running jobs of the resident node table form the victim pool: running
+ * job r uses req[d*R + r] on node[r] with priority prio[r]; its usage must
+ * already be part of the loaded `used` (per node and dim the running requests
+ * sum to <= used), else KP_EINVAL. kp_load_nodes clears the pool.
+ */
+int kp_load_running(kp_ctx *ctx, int32_t R, const int32_t *node, const int64_t *req,
+                    const int32_t *prio);
+
+typedef struct kp_preemption {
+  int32_t *node_of_job;    /* [J] nominated node, -1 = none                   */
+  int32_t *victims_of_job; /* [J] running jobs to evict there, 0 = none       */
+  int64_t *cost_of_job;    /* [J] sum of the victims' priorities, 0 = none    */
+  /* filled by the library: */
+  int32_t preemptors;      /* NO_FIT singleton jobs scored                     */
+  int32_t nominated;       /* preemptors with a candidate node                 */
+  int64_t pairs_scored;    /* preemptors x N                                   */
+} kp_preemption;
+
+/*
+ * After kp_solve: for every NO_FIT job that is a singleton unit (gang size 1)
+ * with priority p, pick the node whose eviction set is smallest when only
+ * running jobs of priority < p may be evicted (kube-scheduler's
+ * selectVictimsOnNode "reprieve" order: priority desc, running index asc),
+ * against the post-solve usage; ties by lower sum of victim priorities, then
+ * lower node index. Nominations are independent per job (nothing is evicted);
+ * any output array may be NULL.
+ */
+int kp_preempt(kp_ctx *ctx, kp_preemption *out);
+
 /* Timing of the last kp_solve, measured with HIP events on the solve stream. */
 typedef struct kp_timing {
   double solve_ms;          /* whole device solve (first launch .. last)     */

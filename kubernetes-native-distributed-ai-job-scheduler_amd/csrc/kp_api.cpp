@@ -88,6 +88,7 @@ static int ensure_nodes(kp_ctx *c, int32_t N, int32_t D) {
   KP_TRY(dalloc(&c->d.topo, (size_t)n));
   KP_TRY(dalloc(&c->d.seg_start, (size_t)n));
   KP_TRY(dalloc(&c->d.seg_end, (size_t)n));
+  KP_TRY(dalloc(&c->d.roff, (size_t)n + 1));
   c->cap_N = n;
   return KP_OK;
 }
@@ -110,6 +111,8 @@ static int ensure_units(kp_ctx *c, int32_t U, int32_t J) {
     KP_TRY(dalloc(&c->d.gpart, pm));
     KP_TRY(dalloc(&c->d.nparts, u));
     KP_TRY(dalloc(&c->d.arrive, u));
+    KP_TRY(dalloc(&c->d.uprio, u));
+    KP_TRY(dalloc(&c->d.plist, u));
     KP_TRY(dalloc(&c->d.win, pm / 64 + 128));
     KP_TRY(dalloc(&c->d.inv, pm));
     KP_TRY(dalloc(&c->d.ent_unit, pm));
@@ -142,6 +145,9 @@ static int ensure_units(kp_ctx *c, int32_t U, int32_t J) {
     KP_TRY(dalloc(&c->d.job_node, j));
     KP_TRY(dalloc(&c->d.job_score, j));
     KP_TRY(dalloc(&c->d.job_status, j));
+    KP_TRY(dalloc(&c->d.pre_node, j));
+    KP_TRY(dalloc(&c->d.pre_vict, j));
+    KP_TRY(dalloc(&c->d.pre_cost, j));
     c->cap_J = (int32_t)j;
   }
   return KP_OK;
@@ -306,7 +312,8 @@ void kp_destroy(kp_ctx *c) {
                   d.ent_slot, d.ent_size, d.ent_lead, d.ent_q,
                   d.csr_kin, d.csr_vin,
                   d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
-                  d.temp, d.xg_counts, d.xg_send, d.xg_recv};
+                  d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.roff,
+                  d.rreq, d.rsuf, d.rprio, d.pre_node, d.pre_vict, d.pre_cost};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->world > 1) {
@@ -372,6 +379,9 @@ int kp_load_nodes(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap, const int
     KP_HIP(hipMemcpyAsync(c->d.topo, c->h_topo.data(), sizeof(int32_t) * N,
                           hipMemcpyHostToDevice, c->stream));
   }
+  // the victim pool belongs to the previous node table
+  c->R = 0;
+  KP_HIP(hipMemsetAsync(c->d.roff, 0, sizeof(int32_t) * ((size_t)N + 1), c->stream));
   KP_HIP(hipStreamSynchronize(c->stream));
   c->util_scale_loaded = 0;  // force an R rebuild at the next solve
   c->cap_rows = c->d.score ? c->cap_rows : 0;
@@ -435,10 +445,12 @@ int kp_load_jobs(kp_ctx *c, int32_t J, const int64_t *req, const int32_t *prio,
                      [&](int32_t a, int32_t b) { return uprio[a] > uprio[b]; });
     c->h_leader.resize(U);
     c->h_size.resize(U);
+    c->h_prio.resize(U);
     c->h_q.resize((size_t)D * U);
     for (int32_t r = 0; r < U; ++r) {
       c->h_leader[r] = leader[ord[r]];
       c->h_size[r] = size[ord[r]];
+      c->h_prio[r] = uprio[ord[r]];
       for (int d = 0; d < D; ++d)
         c->h_q[(size_t)d * U + r] = req[(int64_t)d * J + leader[ord[r]]];
     }
@@ -456,6 +468,8 @@ int kp_load_jobs(kp_ctx *c, int32_t J, const int64_t *req, const int32_t *prio,
     KP_HIP(hipMemcpyAsync(c->d.size, c->h_size.data(), sizeof(int32_t) * c->U,
                           hipMemcpyHostToDevice, c->stream));
     KP_HIP(hipMemcpyAsync(c->d.q, c->h_q.data(), sizeof(int64_t) * D * c->U,
+                          hipMemcpyHostToDevice, c->stream));
+    KP_HIP(hipMemcpyAsync(c->d.uprio, c->h_prio.data(), sizeof(int32_t) * c->U,
                           hipMemcpyHostToDevice, c->stream));
   }
   KP_HIP(hipStreamSynchronize(c->stream));
@@ -775,6 +789,113 @@ int kp_score(kp_ctx *c, const kp_params *p, int32_t job_lo, int32_t job_hi, int3
       if (mask) std::memcpy(mask + (r0 + r) * uw, hm.data() + (size_t)r * words, sizeof(uint64_t) * uw);
     }
   }
+  return KP_OK;
+}
+
+int kp_load_running(kp_ctx *c, int32_t R, const int32_t *node, const int64_t *req,
+                    const int32_t *prio) {
+  if (!c) return KP_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->nodes_loaded) return KP_ESTATE;
+  if (R < 0 || (R > 0 && (!node || !req || !prio))) return KP_EINVAL;
+  const int32_t N = c->N, D = c->D;
+  std::vector<int32_t> ord, off;
+  std::vector<int64_t> sum, rreq, rsuf;
+  std::vector<int32_t> rprio;
+  try {
+    // validation identical to oracle kpo_check_running: running usage is part
+    // of the loaded `used`
+    sum.assign((size_t)D * N + 1, 0);
+    for (int32_t r = 0; r < R; ++r) {
+      const int32_t n = node[r];
+      if (n < 0 || n >= N) return KP_EINVAL;
+      for (int d = 0; d < D; ++d) {
+        const int64_t q = req[(int64_t)d * R + r];
+        if (q < 0 || q > KP_MAX_VALUE) return KP_EINVAL;
+        if ((sum[(size_t)d * N + n] += q) > c->h_used[(size_t)d * N + n]) return KP_EINVAL;
+      }
+    }
+    // node-major CSR in reprieve order: (node, prio desc, running index asc)
+    ord.resize(R);
+    for (int32_t r = 0; r < R; ++r) ord[r] = r;
+    std::sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) {
+      if (node[a] != node[b]) return node[a] < node[b];
+      if (prio[a] != prio[b]) return prio[a] > prio[b];
+      return a < b;
+    });
+    off.assign((size_t)N + 1, 0);
+    for (int32_t r = 0; r < R; ++r) off[node[r] + 1]++;
+    for (int32_t n = 0; n < N; ++n) off[n + 1] += off[n];
+    rreq.resize((size_t)D * R);
+    rsuf.resize((size_t)D * R);
+    rprio.resize(R);
+    for (int32_t e = 0; e < R; ++e) {
+      rprio[e] = prio[ord[e]];
+      for (int d = 0; d < D; ++d) rreq[(size_t)d * R + e] = req[(int64_t)d * R + ord[e]];
+    }
+    // suffix sums of the requests within each node's segment
+    for (int32_t n = 0; n < N; ++n)
+      for (int d = 0; d < D; ++d) {
+        int64_t acc = 0;
+        for (int32_t e = off[n + 1] - 1; e >= off[n]; --e) {
+          acc += rreq[(size_t)d * R + e];
+          rsuf[(size_t)d * R + e] = acc;
+        }
+      }
+  } catch (const std::bad_alloc &) {
+    return KP_ENOMEM;
+  }
+  KP_HIP(hipSetDevice(c->device));
+  if (R > c->cap_R) {
+    KP_TRY(dalloc(&c->d.rreq, (size_t)D * R));
+    KP_TRY(dalloc(&c->d.rsuf, (size_t)D * R));
+    KP_TRY(dalloc(&c->d.rprio, (size_t)R));
+    c->cap_R = R;
+  }
+  if (R > 0) {
+    KP_HIP(hipMemcpyAsync(c->d.rreq, rreq.data(), sizeof(int64_t) * D * R, hipMemcpyHostToDevice,
+                          c->stream));
+    KP_HIP(hipMemcpyAsync(c->d.rsuf, rsuf.data(), sizeof(int64_t) * D * R, hipMemcpyHostToDevice,
+                          c->stream));
+    KP_HIP(hipMemcpyAsync(c->d.rprio, rprio.data(), sizeof(int32_t) * R, hipMemcpyHostToDevice,
+                          c->stream));
+  }
+  KP_HIP(hipMemcpyAsync(c->d.roff, off.data(), sizeof(int32_t) * ((size_t)N + 1),
+                        hipMemcpyHostToDevice, c->stream));
+  KP_HIP(hipStreamSynchronize(c->stream));
+  c->R = R;
+  return KP_OK;
+}
+
+int kp_preempt(kp_ctx *c, kp_preemption *out) {
+  if (!c || !out) return KP_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->solved) return KP_ESTATE;
+  KP_HIP(hipSetDevice(c->device));
+  int32_t P = 0;
+  KP_TRY(launch_preempt(c, &P));
+  const int32_t J = c->J;
+  if (J > 0) {
+    if (out->node_of_job)
+      KP_HIP(hipMemcpyAsync(out->node_of_job, c->d.pre_node, sizeof(int32_t) * J,
+                            hipMemcpyDeviceToHost, c->stream));
+    if (out->victims_of_job)
+      KP_HIP(hipMemcpyAsync(out->victims_of_job, c->d.pre_vict, sizeof(int32_t) * J,
+                            hipMemcpyDeviceToHost, c->stream));
+    if (out->cost_of_job)
+      KP_HIP(hipMemcpyAsync(out->cost_of_job, c->d.pre_cost, sizeof(int64_t) * J,
+                            hipMemcpyDeviceToHost, c->stream));
+  }
+  std::vector<int32_t> nom(J > 0 ? J : 1);
+  if (J > 0)
+    KP_HIP(hipMemcpyAsync(nom.data(), c->d.pre_node, sizeof(int32_t) * J, hipMemcpyDeviceToHost,
+                          c->stream));
+  KP_HIP(hipStreamSynchronize(c->stream));
+  int32_t n_nom = 0;
+  for (int32_t j = 0; j < J; ++j) n_nom += nom[j] >= 0;
+  out->preemptors = P;
+  out->nominated = n_nom;
+  out->pairs_scored = (int64_t)P * c->N;
   return KP_OK;
 }
 

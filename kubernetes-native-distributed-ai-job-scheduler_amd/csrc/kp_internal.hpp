@@ -78,6 +78,15 @@ struct DevState {
   int64_t *ent_q = nullptr;     // [D][U*K] request of the entry's unit
   int32_t *seg_start = nullptr, *seg_end = nullptr;  // [N]
   int32_t *pass_flag = nullptr; // [64] pass p produced proposals
+  // preemption: unit priorities, victim-pool CSR sorted
+  // (node, prio desc, running index asc) with per-node suffix sums, outputs
+  int32_t *uprio = nullptr;     // [U]
+  int32_t *plist = nullptr;     // [U] preemptor units of the last kp_preempt
+  int32_t *roff = nullptr;      // [N+1]
+  int64_t *rreq = nullptr, *rsuf = nullptr;  // [D][R]
+  int32_t *rprio = nullptr;     // [R]
+  int32_t *pre_node = nullptr, *pre_vict = nullptr;  // [J]
+  int64_t *pre_cost = nullptr;  // [J]
   int32_t *counters = nullptr;  // small device counters
   void *temp = nullptr;         // rocprim temporary storage
   size_t temp_bytes = 0;
@@ -104,7 +113,7 @@ struct kp_ctx {
   int32_t select_lds_cap = 0;
   bool select_generic = false;
   // sizes
-  int32_t N = 0, D = 0, J = 0, U = 0;
+  int32_t N = 0, D = 0, J = 0, U = 0, R = 0, cap_R = 0;
   int32_t cap_N = 0, cap_U = 0, cap_J = 0, cap_rows = 0, cap_props = 0, cap_K = 0;
   int32_t u_lo = 0, u_hi = 0;  // this rank's shard of units (rank positions)
   bool nodes_loaded = false, jobs_loaded = false, solved = false;
@@ -116,7 +125,7 @@ struct kp_ctx {
   // host mirrors
   std::vector<int64_t> h_cap, h_used;
   std::vector<int32_t> h_topo;
-  std::vector<int32_t> h_leader, h_size;
+  std::vector<int32_t> h_leader, h_size, h_prio;
   std::vector<int64_t> h_q;
   // pinned host scratch
   int32_t *pinned = nullptr;  // small counters
@@ -144,6 +153,7 @@ int launch_finalize(kp_ctx *c);
 int launch_pack_exchange(kp_ctx *c, int32_t A, int32_t K);
 int launch_unpack_exchange(kp_ctx *c, int32_t world, int32_t Umax, int32_t K);
 size_t rocprim_temp_bytes(int32_t max_items);
+int launch_preempt(kp_ctx *c, int32_t *P_host);
 }  // namespace kp
 
 #define KP_HIP(expr)                                                \

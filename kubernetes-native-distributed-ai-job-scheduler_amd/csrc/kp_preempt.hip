@@ -1,0 +1,194 @@
+// kp_preempt.hip — gfx950 preemption-candidate scoring (DESIGN.md §2.9,
+// BASELINE config #4), bit-exact with oracle/kp_oracle.c kpo_preempt.
+//
+// Rows = preemptors (NO_FIT singleton units, compacted after the solve),
+// columns = nodes. The victim pool is a node-major CSR of the running jobs,
+// sorted (node, priority desc, running index asc) once at kp_load_running,
+// with per-node suffix sums of their requests so that "free + everything
+// evictable" is one load per dim. A workgroup owns RB preemptor rows and
+// sweeps every node (thread per node, node data re-read from L2 per tile);
+// the reprieve walk is a short per-thread loop over the node's evictable
+// running jobs. Each thread keeps its best (victims, cost, node) per row and
+// the workgroup reduces them lexicographically.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include <rocprim/rocprim.hpp>
+
+#include "kp_device.hpp"
+#include "kp_internal.hpp"
+
+namespace kp {
+namespace {
+using namespace dev;
+
+constexpr int kPreRows = 4;  // preemptor rows per workgroup
+
+struct Best {
+  int32_t cnt;
+  int64_t cost;
+  int32_t node;  // -1 = none
+};
+
+__device__ __forceinline__ bool better(const Best &a, const Best &b) {
+  if (a.node < 0) return false;
+  if (b.node < 0) return true;
+  if (a.cnt != b.cnt) return a.cnt < b.cnt;
+  if (a.cost != b.cost) return a.cost < b.cost;
+  return a.node < b.node;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_preempt(int32_t N, int32_t U, int32_t P, int32_t R,
+                                                 const int32_t *__restrict__ plist,
+                                                 const int64_t *__restrict__ q,
+                                                 const int32_t *__restrict__ uprio,
+                                                 const int32_t *__restrict__ leader,
+                                                 const int64_t *__restrict__ cap,
+                                                 const int64_t *__restrict__ used,
+                                                 const int32_t *__restrict__ roff,
+                                                 const int64_t *__restrict__ rreq,
+                                                 const int64_t *__restrict__ rsuf,
+                                                 const int32_t *__restrict__ rprio,
+                                                 int32_t *__restrict__ out_node,
+                                                 int32_t *__restrict__ out_vict,
+                                                 int64_t *__restrict__ out_cost) {
+  __shared__ int64_t sq[kPreRows][D];
+  __shared__ int32_t spr[kPreRows];
+  __shared__ Best wbest[kPreRows][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r0 = blockIdx.x * kPreRows;
+  const int nrows = min(kPreRows, P - r0);
+  if (tid < nrows * D) {
+    const int rr = tid / D, d = tid % D;
+    sq[rr][d] = q[(int64_t)d * U + plist[r0 + rr]];
+  }
+  if (tid < nrows) spr[tid] = uprio[plist[r0 + tid]];
+  __syncthreads();
+  Best best[kPreRows];
+#pragma unroll
+  for (int rr = 0; rr < kPreRows; ++rr) best[rr] = Best{0, 0, -1};
+  for (int n = tid; n < N; n += 256) {
+    const int32_t e0 = roff[n], e1 = roff[n + 1];
+    int64_t fr[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) fr[d] = cap[(int64_t)d * N + n] - used[(int64_t)d * N + n];
+#pragma unroll
+    for (int rr = 0; rr < kPreRows; ++rr) {
+      if (rr >= nrows) break;
+      const int32_t p = spr[rr];
+      int32_t f = e0;
+      while (f < e1 && rprio[f] >= p) ++f;  // evictable = [f, e1)
+      int64_t av[D];
+      bool ok = true;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        av[d] = fr[d] + (f < e1 ? rsuf[(int64_t)d * R + f] : 0);
+        ok &= sq[rr][d] <= av[d];
+      }
+      if (!ok) continue;
+      int32_t cnt = 0;
+      int64_t cost = 0;
+      for (int32_t e = f; e < e1; ++e) {
+        int64_t x[D];
+        bool spare = true;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          x[d] = rreq[(int64_t)d * R + e];
+          spare &= sq[rr][d] <= av[d] - x[d];
+        }
+        if (spare) {
+#pragma unroll
+          for (int d = 0; d < D; ++d) av[d] -= x[d];
+        } else {
+          ++cnt;
+          cost += rprio[e];
+        }
+      }
+      const Best c{cnt, cost, n};
+      if (better(c, best[rr])) best[rr] = c;  // n ascends per thread: ties keep the earlier
+    }
+  }
+  // workgroup reduction per row: wave butterfly, then the 4 wave results
+#pragma unroll
+  for (int rr = 0; rr < kPreRows; ++rr) {
+    Best b = best[rr];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      Best o;
+      o.cnt = __shfl_xor(b.cnt, m, kWave);
+      o.cost = (int64_t)shfl_xor_u64((uint64_t)b.cost, m);
+      o.node = __shfl_xor(b.node, m, kWave);
+      if (better(o, b)) b = o;
+    }
+    if (lane == 0) wbest[rr][wave] = b;
+  }
+  __syncthreads();
+  if (tid < nrows) {
+    Best b = wbest[tid][0];
+    for (int w = 1; w < 4; ++w)
+      if (better(wbest[tid][w], b)) b = wbest[tid][w];
+    const int32_t j = leader[plist[r0 + tid]];
+    out_node[j] = b.node;
+    out_vict[j] = b.node >= 0 ? b.cnt : 0;
+    out_cost[j] = b.node >= 0 ? b.cost : 0;
+  }
+}
+
+__global__ void k_preempt_flags(const int32_t *__restrict__ status,
+                                const int32_t *__restrict__ size, int32_t U,
+                                int32_t *__restrict__ flag) {
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u < U) flag[u] = (status[u] == kNoFit && size[u] == 1) ? 1 : 0;
+}
+
+__global__ void k_preempt_init(int32_t J, int32_t *__restrict__ node, int32_t *__restrict__ vict,
+                               int64_t *__restrict__ cost) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= J) return;
+  node[j] = -1;
+  vict[j] = 0;
+  cost[j] = 0;
+}
+
+template <int D>
+struct PreemptL {
+  static int run(kp_ctx *c, int32_t P) {
+    hipLaunchKernelGGL((k_preempt<D>), dim3(blocks(P, kPreRows)), dim3(256), 0, c->stream, c->N,
+                       c->U, P, c->R, c->d.plist, c->d.q, c->d.uprio, c->d.leader, c->d.cap,
+                       c->d.used, c->d.roff, c->d.rreq, c->d.rsuf, c->d.rprio, c->d.pre_node,
+                       c->d.pre_vict, c->d.pre_cost);
+    KP_HIP(hipGetLastError());
+    return KP_OK;
+  }
+};
+
+}  // namespace
+
+// preemptor compaction (NO_FIT singletons, rank order) -> count to host
+int launch_preempt(kp_ctx *c, int32_t *P_host) {
+  *P_host = 0;
+  const int32_t U = c->U, J = c->J;
+  if (J > 0) {
+    hipLaunchKernelGGL(k_preempt_init, dim3(blocks(J, 256)), dim3(256), 0, c->stream, J,
+                       c->d.pre_node, c->d.pre_vict, c->d.pre_cost);
+    KP_HIP(hipGetLastError());
+  }
+  if (U == 0) return KP_OK;
+  hipLaunchKernelGGL(k_preempt_flags, dim3(blocks(U, 256)), dim3(256), 0, c->stream, c->d.status,
+                     c->d.size, U, c->d.flag);
+  KP_HIP(hipGetLastError());
+  size_t tb = c->d.temp_bytes;
+  KP_HIP(rocprim::select(c->d.temp, tb, rocprim::counting_iterator<int32_t>(0), c->d.flag,
+                         c->d.plist, c->d.counters, (size_t)U, c->stream));
+  KP_HIP(hipMemcpyAsync(c->pinned, c->d.counters, sizeof(int32_t), hipMemcpyDeviceToHost,
+                        c->stream));
+  KP_HIP(hipStreamSynchronize(c->stream));
+  const int32_t P = c->pinned[0];
+  *P_host = P;
+  if (P == 0 || c->N == 0) return KP_OK;
+  return dispatch_D<PreemptL>(c->D, c, P);
+}
+
+}  // namespace kp

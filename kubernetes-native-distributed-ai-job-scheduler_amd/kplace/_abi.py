@@ -81,6 +81,13 @@ class Config(C.Structure):
     ]
 
 
+class Preemption(C.Structure):
+    _fields_ = [
+        ("node_of_job", _i32p), ("victims_of_job", _i32p), ("cost_of_job", _i64p),
+        ("preemptors", C.c_int32), ("nominated", C.c_int32), ("pairs_scored", C.c_int64),
+    ]
+
+
 class Timing(C.Structure):
     _fields_ = [
         ("solve_ms", C.c_double), ("score_ms", C.c_double),
@@ -158,6 +165,8 @@ def load_library(path: str | None = None) -> C.CDLL:
         "kp_last_timing": (C.c_int, [vp, C.POINTER(Timing)]),
         "kp_set_profiling": (C.c_int, [vp, C.c_int]),
         "kp_parse_gpu_memory": (C.c_int, [C.c_char_p, _i64p]),
+        "kp_load_running": (C.c_int, [vp, C.c_int32, _i32p, _i64p, _i32p]),
+        "kp_preempt": (C.c_int, [vp, C.POINTER(Preemption)]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -171,5 +180,6 @@ EXPORTED = (
     "kp_params_default", "kp_create", "kp_destroy", "kp_strerror",
     "kp_abi_version", "kp_dist_unique_id", "kp_place", "kp_load_nodes",
     "kp_load_jobs", "kp_solve", "kp_fetch", "kp_apply_delta", "kp_reset_nodes", "kp_score",
-    "kp_last_timing", "kp_set_profiling", "kp_parse_gpu_memory",
+    "kp_last_timing", "kp_set_profiling", "kp_parse_gpu_memory", "kp_load_running",
+    "kp_preempt",
 )

@@ -136,6 +136,24 @@ class Placer:
         _check(lib().kp_apply_delta(self._h, _ptr(node_idx, C.c_int32), _ptr(delta, C.c_int64), K),
                "kp_apply_delta")
 
+    def load_running(self, node, req, prio) -> None:
+        """kp_load_running: the victim pool (running jobs) of the resident
+        node table, req [D, R]."""
+        node, req, prio = _c(node, np.int32), _c(req, np.int64), _c(prio, np.int32)
+        R = node.shape[0]
+        _check(lib().kp_load_running(self._h, R, _ptr(node, C.c_int32), _ptr(req, C.c_int64),
+                                     _ptr(prio, C.c_int32)), "kp_load_running")
+
+    def preempt(self) -> dict:
+        """kp_preempt after a solve: per-job nominated node / victims / cost."""
+        node = np.empty(self.J, np.int32)
+        vict = np.empty(self.J, np.int32)
+        cost = np.empty(self.J, np.int64)
+        r = _abi.Preemption(_ptr(node, C.c_int32), _ptr(vict, C.c_int32), _ptr(cost, C.c_int64))
+        _check(lib().kp_preempt(self._h, C.byref(r)), "kp_preempt")
+        return dict(node=node, victims=vict, cost=cost, preemptors=r.preemptors,
+                    nominated=r.nominated, pairs=r.pairs_scored)
+
     def reset_nodes(self) -> None:
         _check(lib().kp_reset_nodes(self._h), "kp_reset_nodes")
 

@@ -130,10 +130,84 @@ def config3(J: int = 100_000, N: int = 10_000) -> Workload:
                     name=f"config3_{J}x{N}")
 
 
+def prefill_running(seed: int, cap: np.ndarray, occupancy: float, probes: int = 64):
+    """Pre-place synthetic running jobs (the victim pool of config #4).
+
+    Running job k draws its request and priority like a pending job (seed +
+    0x1000, so the draws are independent of the queue) and a start node
+    x mod N (stream 2); it goes to the first node of start, start+1, ...
+    (at most `probes`) where it fits, or is dropped. Jobs are added until the
+    GPU-count dimension reaches `occupancy` of its capacity (SURVEY §8d asks
+    >= 30% per dim; with this job mix GPUs saturate long before memory reaches
+    30%: a job takes ~28% of a mean node's GPUs but ~6% of its memory, so the
+    per-dim rule is unreachable and the scarce GPU dimension sets the level).
+    Returns (used [D, N], node [R], req [D, R], prio [R])."""
+    D_, N = cap.shape
+    used = np.zeros_like(cap)
+    target = occupancy * cap[2].sum()
+    rs = seed + 0x1000
+    nodes, reqs, prios = [], [], []
+    k = 0
+    batch = 4096
+    while used[2].sum() < target and k < 20 * N:
+        _, rq, pr = make_crs(rs, k + batch, gangs=False)
+        starts = (splitmix64(rs, 2, np.arange(k, k + batch, dtype=np.uint64))
+                  % np.uint64(N)).astype(np.int64)
+        for i in range(batch):
+            if used[2].sum() >= target:
+                break
+            q = rq[:, k + i]
+            cand = (starts[i] + np.arange(probes)) % N
+            fits = np.all(used[:, cand] + q[:, None] <= cap[:, cand], axis=0)
+            hit = np.flatnonzero(fits)
+            if hit.size:
+                n = int(cand[hit[0]])
+                used[:, n] += q
+                nodes.append(n)
+                reqs.append(q)
+                prios.append(int(pr[k + i]))
+        k += batch
+    req = np.ascontiguousarray(np.array(reqs, np.int64).T.reshape(D_, len(reqs)))
+    return used, np.array(nodes, np.int32), req, np.array(prios, np.int32)
+
+
+def config4(J: int = 200_000, N: int = 20_000, occupancy: float = 0.30) -> Workload:
+    """#4: priority tiers 0-3 against a cluster pre-filled with running jobs
+    (priorities 0-3; the victim pool for preemption scoring, w.meta['run_*'])
+    up to `occupancy` of its GPUs. Singletons (one pod each), shapes A-D."""
+    seed = SEED_BASE + 4
+    cap, topo = make_nodes(seed, N, ab_only=False)
+    size, req_cr, prio_cr = make_crs(seed, J, gangs=False)
+    req, prio, gid, gsz = expand_crs(J, size, req_cr, prio_cr, gangs=False)
+    used, rnode, rreq, rprio = prefill_running(seed, cap, occupancy)
+    return Workload(J, N, D, req, cap, used, prio, gid, gsz, topo, name=f"config4_{J}x{N}",
+                    meta=dict(run_node=rnode, run_req=rreq, run_prio=rprio))
+
+
+def config5_trace(total: int = 1_000_000, N: int = 50_000):
+    """#5: the streaming trace — a 1M-job queue (singletons, prio 0-3) and a
+    50k-node cluster. Returns (cap, topo, req [D, total], prio [total])."""
+    seed = SEED_BASE + 5
+    cap, topo = make_nodes(seed, N, ab_only=False)
+    size, req_cr, prio_cr = make_crs(seed, total, gangs=False)
+    req, prio, _, _ = expand_crs(total, size, req_cr, prio_cr, gangs=False)
+    return cap, topo, req, prio
+
+
+def config5_completions(batch_no: int, running_jobs: np.ndarray) -> np.ndarray:
+    """Deterministic 20% of the running (previously placed) trace jobs that
+    complete after micro-batch `batch_no`: splitmix64(seed, 3 + batch, job)
+    mod 5 == 0. Returns a boolean mask over `running_jobs` (trace indices)."""
+    x = splitmix64(SEED_BASE + 5, 3 + batch_no, running_jobs.astype(np.uint64))
+    return (x % np.uint64(5)) == np.uint64(0)
+
+
 # scoring knobs per config (DESIGN.md §2.7)
 CONFIG_PARAMS = {
     2: dict(w_dim=(1, 1, 1, 1), w_gpu_fit=0, w_spread=0),
     3: dict(w_dim=(1, 1, 4, 2), w_gpu_fit=1024, w_spread=256),
+    4: dict(w_dim=(1, 1, 4, 2), w_gpu_fit=1024, w_spread=0),
+    5: dict(w_dim=(1, 1, 4, 2), w_gpu_fit=1024, w_spread=0),
 }
 
 
@@ -142,4 +216,6 @@ def config(no: int, J: int | None = None, N: int | None = None) -> Workload:
         return config2(J or 10_000, N or 1_000)
     if no == 3:
         return config3(J or 100_000, N or 10_000)
+    if no == 4:
+        return config4(J or 200_000, N or 20_000)
     raise ValueError(f"config #{no} generator not implemented")

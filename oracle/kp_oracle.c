@@ -36,6 +36,7 @@ struct kpo_state {
   int32_t *size;      /* [U] members                                         */
   uint32_t *salt;     /* [U] rotated tie-break salt (§2.3)                   */
   int32_t *status;    /* [U] ACTIVE / PLACED / NO_FIT                        */
+  int32_t *prio;      /* [U] unit priority                                   */
   int32_t *job_node;  /* [J]                                                 */
   int32_t *job_score; /* [J]                                                 */
   int32_t rounds;
@@ -136,7 +137,7 @@ void kpo_state_free(kpo_state *st) {
   if (!st) return;
   free(st->used); free(st->topo); free(st->R); free(st->base);
   free(st->leader); free(st->size); free(st->salt);
-  free(st->status); free(st->job_node); free(st->job_score);
+  free(st->status); free(st->prio); free(st->job_node); free(st->job_score);
   free(st);
 }
 
@@ -221,9 +222,10 @@ int kpo_state_new(const kp_snapshot *s, const kp_params *p, kpo_state **out) {
   st->U = U;
   XALLOC(st->leader, U, int32_t); XALLOC(st->size, U, int32_t);
   XALLOC(st->salt, U, uint32_t); XALLOC(st->status, U, int32_t);
+  XALLOC(st->prio, U, int32_t);
   for (int32_t r = 0; r < U; ++r) {
     int32_t u = ord[r];
-    st->leader[r] = uleader[u]; st->size[r] = usize[u];
+    st->leader[r] = uleader[u]; st->size[r] = usize[u]; st->prio[r] = uprio[u];
     st->salt[r] = fmix32((uint32_t)uleader[u] ^ p->tie_seed);
     st->status[r] = ACTIVE;
   }
@@ -475,6 +477,133 @@ int kpo_score(const kp_snapshot *s, const kp_params *p, int32_t job_lo,
       if (mask && sc >= 0) mask[row * words + n / 64] |= (uint64_t)1 << (n % 64);
     }
   }
+  kpo_state_free(st);
+  return KP_OK;
+}
+
+/* ---- §2.9 preemption candidates (BASELINE config #4) ----------------------
+ * The victim pool is the running jobs of the snapshot. For a NO_FIT singleton
+ * unit of priority p and request q, on node n: V = running jobs on n with
+ * priority < p in (priority desc, running index asc) order — the order in which
+ * kube-scheduler's selectVictimsOnNode tries to reprieve them; n qualifies iff
+ * q <= free + sum(V) in every dim (free = cap - post-solve used); walking V,
+ * a job is spared if q still fits without its resources, else it is a victim.
+ * Best node: fewest victims, then lowest sum of victim priorities, then
+ * lowest node index. */
+typedef struct {
+  int32_t node, idx, prio;
+} run_ref;
+
+static int cmp_run(const void *a, const void *b) {
+  const run_ref *x = (const run_ref *)a, *y = (const run_ref *)b;
+  if (x->node != y->node) return x->node < y->node ? -1 : 1;
+  if (x->prio != y->prio) return x->prio > y->prio ? -1 : 1; /* prio desc */
+  return x->idx < y->idx ? -1 : (x->idx > y->idx);
+}
+
+int kpo_check_running(const kp_snapshot *s, int32_t R, const int32_t *node,
+                      const int64_t *req, const int32_t *prio) {
+  if (R < 0 || (R > 0 && (!node || !req || !prio))) return KP_EINVAL;
+  const int32_t N = s->N, D = s->D;
+  int64_t *sum = (int64_t *)calloc((size_t)D * N + 1, sizeof(int64_t));
+  if (!sum) return KP_ENOMEM;
+  int rc = KP_OK;
+  for (int32_t r = 0; r < R && !rc; ++r) {
+    const int32_t n = node[r];
+    if (n < 0 || n >= N) { rc = KP_EINVAL; break; }
+    for (int d = 0; d < D && !rc; ++d) {
+      const int64_t q = req[(int64_t)d * R + r];
+      const int64_t u = s->used ? s->used[(int64_t)d * N + n] : 0;
+      if (q < 0 || q > KP_MAX_VALUE) rc = KP_EINVAL;
+      else if ((sum[(int64_t)d * N + n] += q) > u) rc = KP_EINVAL; /* stays <= 2^57 */
+    }
+  }
+  free(sum);
+  return rc;
+}
+
+int kpo_preempt(const kp_snapshot *s, const kp_params *p, int32_t R, const int32_t *node,
+                const int64_t *req, const int32_t *prio, kp_result *res,
+                kp_preemption *pr, int nthreads) {
+  kpo_state *st;
+  int rc = kpo_state_new(s, p, &st);
+  if (rc) return rc;
+  if ((rc = kpo_check_running(s, R, node, req, prio))) { kpo_state_free(st); return rc; }
+  int32_t *cand;
+  XALLOC(cand, (size_t)st->U * p->n_cand, int32_t);
+  run_ref *rr;
+  int32_t *off;
+  XALLOC(rr, R, run_ref);
+  off = (int32_t *)calloc((size_t)s->N + 2, sizeof(int32_t));
+  if (!cand || !rr || !off) { free(cand); free(rr); free(off); kpo_state_free(st); return KP_ENOMEM; }
+  while (kpo_state_active(st) > 0) { /* the placement itself, as kpo_place */
+    if (p->max_rounds > 0 && st->rounds >= p->max_rounds) break;
+    kpo_round_candidates(st, 0, st->U, cand, nthreads);
+    kpo_round_run(st, cand);
+  }
+  if (res) kpo_state_result(st, res);
+  const int32_t N = st->N, D = st->D, J = st->J;
+  for (int32_t r = 0; r < R; ++r) { rr[r].node = node[r]; rr[r].idx = r; rr[r].prio = prio[r]; }
+  qsort(rr, R, sizeof *rr, cmp_run);
+  for (int32_t r = 0; r < R; ++r) off[rr[r].node + 1]++;
+  for (int32_t n = 0; n < N; ++n) off[n + 1] += off[n];
+  for (int32_t j = 0; j < J; ++j) {
+    if (pr->node_of_job) pr->node_of_job[j] = -1;
+    if (pr->victims_of_job) pr->victims_of_job[j] = 0;
+    if (pr->cost_of_job) pr->cost_of_job[j] = 0;
+  }
+  int32_t npre = 0, nnom = 0;
+  (void)nthreads;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 8) reduction(+ : npre, nnom) \
+    num_threads(nthreads > 0 ? nthreads : 1)
+#endif
+  for (int32_t u = 0; u < st->U; ++u) {
+    if (st->status[u] != NO_FIT || st->size[u] != 1) continue;
+    ++npre;
+    int64_t q[KP_MAX_DIMS], avail[KP_MAX_DIMS];
+    unit_req(st, u, q);
+    const int32_t pu = st->prio[u];
+    int32_t best_n = -1, best_c = 0;
+    int64_t best_cost = 0;
+    for (int32_t n = 0; n < N; ++n) {
+      int32_t f = off[n];
+      const int32_t e1 = off[n + 1];
+      while (f < e1 && rr[f].prio >= pu) ++f; /* V = [f, e1) */
+      int ok = 1;
+      for (int d = 0; d < D; ++d) {
+        avail[d] = st->cap[(int64_t)d * N + n] - st->used[(int64_t)d * N + n];
+        for (int32_t e = f; e < e1; ++e) avail[d] += req[(int64_t)d * R + rr[e].idx];
+        if (q[d] > avail[d]) ok = 0;
+      }
+      if (!ok) continue;
+      int32_t cnt = 0;
+      int64_t cost = 0;
+      for (int32_t e = f; e < e1; ++e) {
+        int spare = 1;
+        for (int d = 0; d < D; ++d)
+          if (q[d] > avail[d] - req[(int64_t)d * R + rr[e].idx]) spare = 0;
+        if (spare) {
+          for (int d = 0; d < D; ++d) avail[d] -= req[(int64_t)d * R + rr[e].idx];
+        } else {
+          ++cnt;
+          cost += rr[e].prio;
+        }
+      }
+      if (best_n < 0 || cnt < best_c || (cnt == best_c && cost < best_cost)) {
+        best_n = n; best_c = cnt; best_cost = cost;
+      }
+    }
+    if (best_n >= 0) ++nnom;
+    const int32_t j = st->leader[u];
+    if (pr->node_of_job) pr->node_of_job[j] = best_n;
+    if (pr->victims_of_job) pr->victims_of_job[j] = best_n >= 0 ? best_c : 0;
+    if (pr->cost_of_job) pr->cost_of_job[j] = best_n >= 0 ? best_cost : 0;
+  }
+  pr->preemptors = npre;
+  pr->nominated = nnom;
+  pr->pairs_scored = (int64_t)npre * N;
+  free(cand); free(rr); free(off);
   kpo_state_free(st);
   return KP_OK;
 }

@@ -35,6 +35,16 @@ int kpo_place(const kp_snapshot *s, const kp_params *p, kp_result *r,
 int kpo_score(const kp_snapshot *s, const kp_params *p, int32_t job_lo,
               int32_t job_hi, int32_t *score, uint64_t *mask);
 
+/* Placement (as kpo_place, outputs into *res if non-NULL) followed by the
+   preemption candidates of DESIGN.md §2.9 against the post-solve usage; the
+   running jobs are (node[r], req[d*R + r], prio[r]). Same validation as
+   kp_load_running. */
+int kpo_preempt(const kp_snapshot *s, const kp_params *p, int32_t R, const int32_t *node,
+                const int64_t *req, const int32_t *prio, kp_result *res,
+                kp_preemption *pr, int nthreads);
+int kpo_check_running(const kp_snapshot *s, int32_t R, const int32_t *node,
+                      const int64_t *req, const int32_t *prio);
+
 /* ---- stepwise interface (world_size>1 protocol tests, tests/test_dist) ---- */
 typedef struct kpo_state kpo_state;
 

@@ -55,6 +55,8 @@ def lib() -> C.CDLL:
         L.kpo_round_run.argtypes = [vp, C.POINTER(C.c_int32)]
         L.kpo_round_run.restype = C.c_int32
         L.kpo_state_result.argtypes = [vp, R]
+        L.kpo_preempt.argtypes = [S, P, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int64),
+                                  C.POINTER(C.c_int32), R, C.POINTER(_abi.Preemption), C.c_int]
         _lib = L
     return _lib
 
@@ -126,3 +128,23 @@ def score(sb: SnapshotBuf, params, lo: int, hi: int):
     if rc != 0:
         return rc
     return sc, mk
+
+
+def preempt(sb: SnapshotBuf, params, run_node, run_req, run_prio, nthreads: int = 1):
+    """Placement + preemption candidates. Returns
+    (placement dict, preemption dict) or the error code."""
+    run_node = np.ascontiguousarray(run_node, dtype=np.int32)
+    run_req = np.ascontiguousarray(run_req, dtype=np.int64)
+    run_prio = np.ascontiguousarray(run_prio, dtype=np.int32)
+    rb = ResultBuf(sb.J, sb.D, sb.N)
+    node = np.full(sb.J, -7, np.int32)
+    vict = np.full(sb.J, -7, np.int32)
+    cost = np.full(sb.J, -7, np.int64)
+    pr = _abi.Preemption(_p(node, C.c_int32), _p(vict, C.c_int32), _p(cost, C.c_int64))
+    rc = lib().kpo_preempt(C.byref(sb.snap), C.byref(params), run_node.shape[0],
+                           _p(run_node, C.c_int32), _p(run_req, C.c_int64),
+                           _p(run_prio, C.c_int32), C.byref(rb.res), C.byref(pr), nthreads)
+    if rc != 0:
+        return rc
+    return rb.as_dict(), dict(node=node, victims=vict, cost=cost, preemptors=pr.preemptors,
+                              nominated=pr.nominated, pairs=pr.pairs_scored)

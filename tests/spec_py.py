@@ -161,3 +161,46 @@ def place(req, cap, used, prio, gang_id, topo, p):
                 job_score[ld + m] = -1
     return dict(node=job_node, score=job_score, status=out_status, used=used,
                 rounds=rounds, passes=passes)
+
+
+def preempt(req, cap, used_after, prio, status, singleton, run_node, run_req, run_prio):
+    """Preemption candidates, restated from the spec text:
+    for each NO_FIT singleton job, every node's evictable running jobs
+    (priority below the job's) in (priority desc, index asc) reprieve order;
+    best node by (victims, sum of victim priorities, node index).
+    Returns (node, victims, cost) lists over jobs."""
+    D = len(cap)
+    N = len(cap[0]) if D else 0
+    J = len(prio)
+    R = len(run_node)
+    by_node = {n: [] for n in range(N)}
+    for r in range(R):
+        by_node[int(run_node[r])].append(r)
+    for n in by_node:
+        by_node[n].sort(key=lambda r: (-int(run_prio[r]), r))
+    out_n, out_v, out_c = [-1] * J, [0] * J, [0] * J
+    for j in range(J):
+        if int(status[j]) != 1 or not singleton[j]:   # KP_JOB_NO_FIT, gang size 1
+            continue
+        p = int(prio[j])
+        q = [int(req[d][j]) for d in range(D)]
+        best = None
+        for n in range(N):
+            V = [r for r in by_node[n] if int(run_prio[r]) < p]
+            avail = [int(cap[d][n]) - int(used_after[d][n]) + sum(int(run_req[d][r]) for r in V)
+                     for d in range(D)]
+            if any(q[d] > avail[d] for d in range(D)):
+                continue
+            cnt = cost = 0
+            for r in V:
+                rq = [int(run_req[d][r]) for d in range(D)]
+                if all(q[d] <= avail[d] - rq[d] for d in range(D)):
+                    avail = [avail[d] - rq[d] for d in range(D)]
+                else:
+                    cnt += 1
+                    cost += int(run_prio[r])
+            if best is None or (cnt, cost, n) < best:
+                best = (cnt, cost, n)
+        if best is not None:
+            out_n[j], out_v[j], out_c[j] = best[2], best[0], best[1]
+    return out_n, out_v, out_c

@@ -39,7 +39,8 @@ def test_struct_layouts_match_header(tmp_path):
     """Field offsets of every ctypes mirror equal the C compiler's."""
     import subprocess
     structs = {"kp_snapshot": _abi.Snapshot, "kp_params": _abi.Params, "kp_result": _abi.Result,
-               "kp_config": _abi.Config, "kp_timing": _abi.Timing}
+               "kp_config": _abi.Config, "kp_timing": _abi.Timing,
+               "kp_preemption": _abi.Preemption}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HDR}"', "int main(void){"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')

@@ -280,3 +280,67 @@ def test_streaming_apply_delta(oracle, placer):
         done = done[rng.random(done.size) < 0.2]
         placer.apply_delta(g["node"][done], -req[:, done])
         np.subtract.at(used.T, g["node"][done], req[:, done].T)
+
+
+# ---------------------------------------------------------------------------
+# preemption candidates (kp_load_running + kp_preempt)
+# ---------------------------------------------------------------------------
+def _preempt_both(oracle, placer, w, p, rn, rq, rp):
+    placer.load_nodes(w.cap, w.used, w.topo)
+    placer.load_running(rn, rq, rp)
+    placer.load_jobs(w.req, w.prio, w.gang_id, w.gang_size)
+    placer.solve(p)
+    g = placer.fetch()
+    gp = placer.preempt()
+    o, op = oracle.preempt(_snap(oracle, w), p, rn, rq, rp, nthreads=NTH)
+    return g, gp, o, op
+
+
+def _assert_same_pre(gp, op, ctx=""):
+    for k in ("node", "victims", "cost"):
+        bad = np.nonzero(gp[k] != op[k])[0]
+        assert bad.size == 0, f"{ctx} preempt {k} differs at {bad[:10]}: gpu={gp[k][bad[:10]]} cpu={op[k][bad[:10]]}"
+    for k in ("preemptors", "nominated", "pairs"):
+        assert gp[k] == op[k], f"{ctx} {k}: gpu={gp[k]} cpu={op[k]}"
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_preempt_random_parity(oracle, placer, seed):
+    from test_oracle import rand_running
+    w = random_workload(300 + seed, J=900, N=70 + 13 * seed, used_frac=0.9)
+    rn, rq, rp = rand_running(seed, w, per_node=1 + seed)
+    p = _abi.default_params(tie_mode=seed % 2, score_mode=(seed // 2) % 2)
+    g, gp, o, op = _preempt_both(oracle, placer, w, p, rn, rq, rp)
+    _assert_same(g, o, f"seed {seed}")
+    _assert_same_pre(gp, op, f"seed {seed}")
+
+
+def test_preempt_config4_parity(oracle, placer):
+    """BASELINE config #4 shape at 1/10 size: priority tiers, 30% GPU
+    occupancy of running jobs, preemption candidates for every NO_FIT job."""
+    w = synth.config4(20_000, 2_000)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[4])
+    m = w.meta
+    g, gp, o, op = _preempt_both(oracle, placer, w, p, m["run_node"], m["run_req"], m["run_prio"])
+    _assert_same(g, o, "config4")
+    _assert_same_pre(gp, op, "config4")
+    # properties: nominees are NO_FIT singletons; a victim set is non-empty
+    nom = gp["node"] >= 0
+    assert (g["status"][nom] == _abi.KP_JOB_NO_FIT).all()
+    assert (gp["victims"][nom] >= 1).all()
+
+
+def test_preempt_requires_solve_and_valid_pool(placer):
+    cap = np.full((4, 3), 10, np.int64)
+    used = np.full((4, 3), 5, np.int64)
+    placer.load_nodes(cap, used)
+    with pytest.raises(KPlaceError) as e:
+        placer.load_running(np.array([0], np.int32), np.full((4, 1), 6, np.int64),
+                            np.array([0], np.int32))   # 6 > used 5
+    assert e.value.code == _abi.KP_EINVAL
+    placer.load_running(np.array([0, 2], np.int32), np.full((4, 2), 5, np.int64),
+                        np.array([0, 1], np.int32))
+    placer.load_jobs(np.full((4, 2), 7, np.int64), np.array([3, 0], np.int32))
+    placer.solve(_abi.default_params())
+    pr = placer.preempt()
+    assert pr["node"].tolist() == [0, -1] and pr["victims"].tolist() == [1, 0]

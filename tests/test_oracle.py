@@ -240,3 +240,88 @@ def test_golden_fixture(oracle, path):
 
 def test_golden_present():
     assert len(glob.glob(os.path.join(GOLDEN, "place_*.npz"))) >= 4
+
+
+# ---------------------------------------------------------------------------
+# preemption candidates
+# ---------------------------------------------------------------------------
+def run_pre(oracle, w, p, rn, rq, rp, threads=1):
+    out = oracle.preempt(oracle.SnapshotBuf.from_workload(w), p, rn, rq, rp, nthreads=threads)
+    assert not isinstance(out, int), f"oracle error {out}"
+    return out
+
+
+def test_kat_preempt_fewest_then_cheapest(oracle):
+    # n0 (cap 8, full): running prio 0 (4) and prio 2 (4); n1 (cap 8, full):
+    # running prio 1 (8). A prio-2 job needing 4 fits nowhere; evicting the
+    # prio-0 job on n0 (cost 0) beats evicting the prio-1 job on n1 (cost 1).
+    w = W([[4]], [[8, 8]], used=[[8, 8]], prio=[2])
+    r, pr = run_pre(oracle, w, P(), [0, 0, 1], [[4, 4, 8]], [0, 2, 1])
+    assert r["status"].tolist() == [_abi.KP_JOB_NO_FIT]
+    assert pr["node"].tolist() == [0] and pr["victims"].tolist() == [1]
+    assert pr["cost"].tolist() == [0]
+    assert (pr["preemptors"], pr["nominated"]) == (1, 1)
+
+
+def test_kat_preempt_reprieve(oracle):
+    # two prio-0 jobs of 2 on a full 4-node: the first (lower index) is spared,
+    # the second is evicted; a prio-0 preemptor may evict nobody.
+    w = W([[2, 2]], [[4]], used=[[4]], prio=[1, 0])
+    r, pr = run_pre(oracle, w, P(), [0, 0], [[2, 2]], [0, 0])
+    assert pr["node"].tolist() == [0, -1]
+    assert pr["victims"].tolist() == [1, 0]
+    assert (pr["preemptors"], pr["nominated"]) == (2, 1)
+
+
+def test_preempt_validation(oracle):
+    w = W([[4]], [[8]], used=[[3]], prio=[1])
+    assert oracle.preempt(oracle.SnapshotBuf.from_workload(w), P(), [0], [[4]], [0]) == \
+        _abi.KP_EINVAL  # running usage 4 > used 3
+    assert oracle.preempt(oracle.SnapshotBuf.from_workload(w), P(), [1], [[1]], [0]) == \
+        _abi.KP_EINVAL  # node out of range
+
+
+def rand_running(seed, w, per_node=3):
+    rng = np.random.default_rng(seed)
+    rn, rq, rp = [], [], []
+    used = w.used.copy()
+    for n in range(w.N):
+        for _ in range(int(rng.integers(0, per_node + 1))):
+            q = (used[:, n] * rng.random(w.D) * 0.6).astype(np.int64)
+            rn.append(n)
+            rq.append(q)
+            rp.append(int(rng.integers(0, 4)))
+            used[:, n] -= q
+    rq = np.array(rq, np.int64).T.reshape(w.D, len(rn))
+    return np.array(rn, np.int32), np.ascontiguousarray(rq), np.array(rp, np.int32)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_preempt_matches_python_spec(oracle, seed):
+    w = rand_w(200 + seed, J=50 + 9 * seed, N=8 + seed)
+    w.used = (w.cap * 0.7).astype(np.int64)
+    rn, rq, rp = rand_running(seed, w)
+    p = P(w_dim=(1, 3, 2) + (1,) * 5, tie_mode=seed % 2, n_cand=1 + seed % 4)
+    r, pr = run_pre(oracle, w, p, rn, rq, rp, threads=2)
+    single = [True] * w.J
+    for g in set(w.gang_id.tolist()) - {-1}:
+        idx = np.nonzero(w.gang_id == g)[0]
+        if idx.size > 1:
+            for j in idx:
+                single[j] = False
+    n, v, c = spec_py.preempt(w.req, w.cap, r["used"], w.prio, r["status"], single, rn, rq, rp)
+    assert pr["node"].tolist() == n
+    assert pr["victims"].tolist() == v
+    assert pr["cost"].tolist() == c
+    assert pr["preemptors"] == sum(1 for j in range(w.J) if r["status"][j] == 1 and single[j])
+
+
+def test_config4_generator_occupancy():
+    w = synth.config4(4000, 400)
+    util = w.used.sum(1) / w.cap.sum(1)
+    assert util[2] >= 0.30
+    rn, rq, rp = w.meta["run_node"], w.meta["run_req"], w.meta["run_prio"]
+    back = np.zeros_like(w.used)
+    np.add.at(back.T, rn, rq.T)
+    assert np.array_equal(back, w.used)  # the victim pool is exactly the usage
+    assert rp.min() >= 0 and rp.max() <= 3
