@@ -281,8 +281,9 @@ int kp_create(kp_ctx **out, const kp_config *cfg) {
   if (hipSetDevice(dev) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void **>(&c->pinned), 4096, hipHostMallocDefault) !=
-          hipSuccess) {
-    delete c;
+          hipSuccess ||
+      hipMalloc(reinterpret_cast<void **>(&c->d.dl_bad), 16 * sizeof(int32_t)) != hipSuccess) {
+    kp_destroy(c);
     return KP_EHIP;
   }
   if (c->world > 1) {
@@ -313,7 +314,8 @@ void kp_destroy(kp_ctx *c) {
                   d.csr_kin, d.csr_vin,
                   d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
                   d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.roff,
-                  d.rreq, d.rsuf, d.rprio, d.pre_node, d.pre_vict, d.pre_cost};
+                  d.rreq, d.rsuf, d.rprio, d.pre_node, d.pre_vict, d.pre_cost,
+                  d.dl_node, d.dl_delta, d.dl_bad};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->world > 1) {
@@ -711,29 +713,27 @@ int kp_apply_delta(kp_ctx *c, const int32_t *node_idx, const int64_t *delta, int
   if (!c || K < 0 || (K > 0 && (!node_idx || !delta))) return KP_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   if (!c->nodes_loaded) return KP_ESTATE;
-  KP_HIP(hipSetDevice(c->device));
   const int32_t N = c->N, D = c->D;
-  std::vector<int64_t> used((size_t)D * N);
-  if (N > 0)
-    KP_HIP(hipMemcpyAsync(used.data(), c->d.used, sizeof(int64_t) * D * N, hipMemcpyDeviceToHost,
-                          c->stream));
-  KP_HIP(hipStreamSynchronize(c->stream));
   for (int32_t k = 0; k < K; ++k)
     if (node_idx[k] < 0 || node_idx[k] >= N) return KP_EINVAL;
-  for (int32_t k = 0; k < K; ++k)
-    for (int d = 0; d < D; ++d) {
-      int64_t &u = used[(size_t)d * N + node_idx[k]];
-      const int64_t dv = delta[(int64_t)d * K + k];
-      if (dv > KP_MAX_VALUE || dv < -KP_MAX_VALUE) return KP_EINVAL;
-      u += dv;
-    }
-  for (size_t i = 0; i < used.size(); ++i)
-    if (used[i] < 0 || used[i] > c->h_cap[i]) return KP_EINVAL;
-  if (N > 0)
-    KP_HIP(hipMemcpyAsync(c->d.used, used.data(), sizeof(int64_t) * D * N, hipMemcpyHostToDevice,
-                          c->stream));
-  KP_HIP(hipStreamSynchronize(c->stream));
-  return KP_OK;
+  for (int64_t i = 0; i < (int64_t)D * K; ++i)
+    if (delta[i] > KP_MAX_VALUE || delta[i] < -KP_MAX_VALUE) return KP_EINVAL;
+  if (K == 0) return KP_OK;
+  KP_HIP(hipSetDevice(c->device));
+  // device-side: atomic apply, check the touched entries against [0, cap],
+  // undo on violation (the call is all-or-nothing); one host round trip
+  if (K > c->cap_delta) {
+    KP_TRY(dalloc(&c->d.dl_node, (size_t)K));
+    KP_TRY(dalloc(&c->d.dl_delta, (size_t)D * K));
+    c->cap_delta = K;
+  }
+  KP_HIP(hipMemcpyAsync(c->d.dl_node, node_idx, sizeof(int32_t) * K, hipMemcpyHostToDevice,
+                        c->stream));
+  KP_HIP(hipMemcpyAsync(c->d.dl_delta, delta, sizeof(int64_t) * D * K, hipMemcpyHostToDevice,
+                        c->stream));
+  int32_t bad = 0;
+  KP_TRY(launch_delta(c, K, &bad));
+  return bad ? KP_EINVAL : KP_OK;
 }
 
 int kp_reset_nodes(kp_ctx *c) {
@@ -800,8 +800,18 @@ int kp_load_running(kp_ctx *c, int32_t R, const int32_t *node, const int64_t *re
   if (R < 0 || (R > 0 && (!node || !req || !prio))) return KP_EINVAL;
   const int32_t N = c->N, D = c->D;
   std::vector<int32_t> ord, off;
-  std::vector<int64_t> sum, rreq, rsuf;
+  std::vector<int64_t> sum, rreq, rsuf, cur;
   std::vector<int32_t> rprio;
+  KP_HIP(hipSetDevice(c->device));
+  try {
+    cur.resize((size_t)D * N + 1);
+  } catch (const std::bad_alloc &) {
+    return KP_ENOMEM;
+  }
+  if (N > 0)
+    KP_HIP(hipMemcpyAsync(cur.data(), c->d.used, sizeof(int64_t) * D * N, hipMemcpyDeviceToHost,
+                          c->stream));
+  KP_HIP(hipStreamSynchronize(c->stream));
   try {
     // validation identical to oracle kpo_check_running: running usage is part
     // of the loaded `used`
@@ -812,7 +822,7 @@ int kp_load_running(kp_ctx *c, int32_t R, const int32_t *node, const int64_t *re
       for (int d = 0; d < D; ++d) {
         const int64_t q = req[(int64_t)d * R + r];
         if (q < 0 || q > KP_MAX_VALUE) return KP_EINVAL;
-        if ((sum[(size_t)d * N + n] += q) > c->h_used[(size_t)d * N + n]) return KP_EINVAL;
+        if ((sum[(size_t)d * N + n] += q) > cur[(size_t)d * N + n]) return KP_EINVAL;
       }
     }
     // node-major CSR in reprieve order: (node, prio desc, running index asc)

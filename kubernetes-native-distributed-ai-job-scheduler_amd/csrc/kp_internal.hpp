@@ -87,6 +87,10 @@ struct DevState {
   int32_t *rprio = nullptr;     // [R]
   int32_t *pre_node = nullptr, *pre_vict = nullptr;  // [J]
   int64_t *pre_cost = nullptr;  // [J]
+  // streaming churn (kp_apply_delta)
+  int32_t *dl_node = nullptr;   // [K]
+  int64_t *dl_delta = nullptr;  // [D][K]
+  int32_t *dl_bad = nullptr;    // [16] violation flag (allocated at kp_create)
   int32_t *counters = nullptr;  // small device counters
   void *temp = nullptr;         // rocprim temporary storage
   size_t temp_bytes = 0;
@@ -113,7 +117,7 @@ struct kp_ctx {
   int32_t select_lds_cap = 0;
   bool select_generic = false;
   // sizes
-  int32_t N = 0, D = 0, J = 0, U = 0, R = 0, cap_R = 0;
+  int32_t N = 0, D = 0, J = 0, U = 0, R = 0, cap_R = 0, cap_delta = 0;
   int32_t cap_N = 0, cap_U = 0, cap_J = 0, cap_rows = 0, cap_props = 0, cap_K = 0;
   int32_t u_lo = 0, u_hi = 0;  // this rank's shard of units (rank positions)
   bool nodes_loaded = false, jobs_loaded = false, solved = false;
@@ -154,6 +158,7 @@ int launch_pack_exchange(kp_ctx *c, int32_t A, int32_t K);
 int launch_unpack_exchange(kp_ctx *c, int32_t world, int32_t Umax, int32_t K);
 size_t rocprim_temp_bytes(int32_t max_items);
 int launch_preempt(kp_ctx *c, int32_t *P_host);
+int launch_delta(kp_ctx *c, int32_t K, int32_t *bad_host);
 }  // namespace kp
 
 #define KP_HIP(expr)                                                \

@@ -526,6 +526,31 @@ __global__ void k_pack(int32_t A, int32_t K, const int32_t *__restrict__ act,
   for (int k = 0; k < K; ++k) dst[1 + k] = cand[t * K + k];
 }
 
+// streaming churn: used[d][node[k]] += sign * delta[d*K + k] (int64 atomics,
+// several deltas may hit one node), then a check of every touched entry
+__global__ void k_delta_apply(int32_t K, int32_t N, int32_t D, const int32_t *__restrict__ node,
+                              const int64_t *__restrict__ delta, int64_t sign,
+                              int64_t *__restrict__ used) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)K * D) return;
+  const int32_t d = (int32_t)(t / K), k = (int32_t)(t % K);
+  const int64_t v = sign * delta[t];
+  if (v != 0)
+    atomicAdd(reinterpret_cast<unsigned long long *>(&used[(int64_t)d * N + node[k]]),
+              (unsigned long long)v);
+}
+
+__global__ void k_delta_check(int32_t K, int32_t N, int32_t D, const int32_t *__restrict__ node,
+                              const int64_t *__restrict__ cap, const int64_t *__restrict__ used,
+                              int32_t *__restrict__ bad) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)K * D) return;
+  const int32_t d = (int32_t)(t / K), k = (int32_t)(t % K);
+  const int64_t i = (int64_t)d * N + node[k];
+  const int64_t u = used[i];
+  if (u < 0 || u > cap[i]) *bad = 1;
+}
+
 template <int D>
 struct ScoreL {
   static int run(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
@@ -641,6 +666,28 @@ int launch_active(kp_ctx *c, int32_t lo, int32_t hi, int32_t *A_host) {
                         c->stream));
   KP_HIP(hipStreamSynchronize(c->stream));
   *A_host = c->pinned[0];
+  return KP_OK;
+}
+
+int launch_delta(kp_ctx *c, int32_t K, int32_t *bad_host) {
+  const int64_t n = (int64_t)K * c->D;
+  int32_t *bad = c->d.dl_bad;
+  KP_HIP(hipMemsetAsync(bad, 0, sizeof(int32_t), c->stream));
+  hipLaunchKernelGGL(k_delta_apply, dim3(blocks(n, 256)), dim3(256), 0, c->stream, K, c->N, c->D,
+                     c->d.dl_node, c->d.dl_delta, (int64_t)1, c->d.used);
+  KP_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_delta_check, dim3(blocks(n, 256)), dim3(256), 0, c->stream, K, c->N, c->D,
+                     c->d.dl_node, c->d.cap, c->d.used, bad);
+  KP_HIP(hipGetLastError());
+  KP_HIP(hipMemcpyAsync(c->pinned + 8, bad, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  KP_HIP(hipStreamSynchronize(c->stream));
+  *bad_host = c->pinned[8];
+  if (*bad_host) {  // undo: the call leaves the table unchanged on failure
+    hipLaunchKernelGGL(k_delta_apply, dim3(blocks(n, 256)), dim3(256), 0, c->stream, K, c->N,
+                       c->D, c->d.dl_node, c->d.dl_delta, (int64_t)-1, c->d.used);
+    KP_HIP(hipGetLastError());
+    KP_HIP(hipStreamSynchronize(c->stream));
+  }
   return KP_OK;
 }
 

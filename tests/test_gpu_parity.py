@@ -344,3 +344,56 @@ def test_preempt_requires_solve_and_valid_pool(placer):
     placer.solve(_abi.default_params())
     pr = placer.preempt()
     assert pr["node"].tolist() == [0, -1] and pr["victims"].tolist() == [1, 0]
+
+
+# ---------------------------------------------------------------------------
+# streaming churn (config #5 shape): micro-batches against a resident table
+# ---------------------------------------------------------------------------
+def test_streaming_config5_trace_parity(oracle, placer):
+    """BASELINE config #5 in miniature: a trace replayed in micro-batches; after
+    each batch a deterministic 20% of the running jobs complete (negative
+    kp_apply_delta). The oracle replays the same trace with its own usage."""
+    total, N, B = 12_000, 3_000, 1_000
+    cap, topo, req, prio = synth.config5_trace(total, N)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[5])
+    placer.load_nodes(cap, None, topo)
+    used_o = np.zeros_like(cap)
+    run_node = np.zeros(0, np.int32)
+    run_job = np.zeros(0, np.int64)
+    for b in range(total // B):
+        lo, hi = b * B, (b + 1) * B
+        rq = np.ascontiguousarray(req[:, lo:hi])
+        placer.load_jobs(rq, prio[lo:hi])
+        placer.solve(p)
+        g = placer.fetch()
+        o = oracle.place(oracle.SnapshotBuf(rq, cap, used_o, prio[lo:hi], topo=topo), p, NTH)
+        _assert_same(g, o, f"batch {b}")
+        used_o = o["used"].copy()
+        ok = g["node"] >= 0
+        run_node = np.concatenate([run_node, g["node"][ok]])
+        run_job = np.concatenate([run_job, lo + np.nonzero(ok)[0]])
+        done = synth.config5_completions(b, run_job)
+        placer.apply_delta(run_node[done], -req[:, run_job[done]])
+        np.subtract.at(used_o.T, run_node[done], req[:, run_job[done]].T)
+        run_node, run_job = run_node[~done], run_job[~done]
+    assert np.array_equal(placer.fetch()["used"], used_o)
+
+
+def test_apply_delta_all_or_nothing(placer):
+    cap = np.full((4, 4), 10, np.int64)
+    used = np.full((4, 4), 3, np.int64)
+    placer.load_nodes(cap, used)
+    placer.load_jobs(np.ones((4, 1), np.int64))
+    placer.solve(_abi.default_params())
+    before = placer.fetch()["used"]
+    # node 1 would go to -1 in dim 0: rejected, nothing applied
+    with pytest.raises(KPlaceError) as e:
+        placer.apply_delta(np.array([0, 1, 1], np.int32),
+                           np.array([[-1, -2, -2], [0, 0, 0], [0, 0, 0], [1, 1, 1]], np.int64))
+    assert e.value.code == _abi.KP_EINVAL
+    assert np.array_equal(placer.fetch()["used"], before)
+    with pytest.raises(KPlaceError):
+        placer.apply_delta(np.array([4], np.int32), np.zeros((4, 1), np.int64))  # bad node
+    placer.apply_delta(np.array([2, 2], np.int32), np.full((4, 2), 3, np.int64))
+    after = placer.fetch()["used"]
+    assert (after[:, 2] == before[:, 2] + 6).all()

@@ -9,5 +9,5 @@ echo "pytest rc=$rc"
 timeout -k 10 300 python -u bench.py --out gpurun_out/bench1.json > gpurun_out/bench1.log 2>&1 || exit $?
 echo "bench ok"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --out gpurun_out/prof/bench_prof.json > gpurun_out/prof/bench.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-stream --out gpurun_out/prof/bench_prof.json > gpurun_out/prof/bench.log 2>&1
 echo "rocprof rc=$?"
