@@ -318,7 +318,10 @@ __global__ __launch_bounds__(BS) void k_select_t(ScoreParams sp,
     const uint32_t Tk = ~(uint32_t)T;
     // branch-free test of every held entry -> one bit each; the (rare)
     // survivors are then appended one at a time, re-reading their score
-    uint64_t hits = 0;
+    constexpr int HW = (V4 + 15) / 16;  // 64-bit hit words (16 int4 = 64 entries each)
+    uint64_t hits[HW];
+#pragma unroll
+    for (int hw = 0; hw < HW; ++hw) hits[hw] = 0;
 #pragma unroll
     for (int t = 0; t < V4; ++t) {
       const int32_t sv[4] = {v[t].x, v[t].y, v[t].z, v[t].w};
@@ -328,13 +331,15 @@ __global__ __launch_bounds__(BS) void k_select_t(ScoreParams sp,
       for (int j = 0; j < 4; ++j) {
         const int32_t s = sv[j];
         const bool h = (s > Ts) | ((s == Ts) & (tj[j] <= Tk));
-        hits |= (uint64_t)(h & (s >= 0)) << (4 * t + j);
+        hits[t >> 4] |= (uint64_t)(h & (s >= 0)) << (4 * (t & 15) + j);
       }
     }
-    while (hits) {
-      const int bpos = __ffsll((unsigned long long)hits) - 1;
-      hits &= hits - 1;
-      const int t = bpos >> 2, j = bpos & 3;
+#pragma unroll
+    for (int hw = 0; hw < HW; ++hw)
+    while (hits[hw]) {
+      const int bpos = __ffsll((unsigned long long)hits[hw]) - 1;
+      hits[hw] &= hits[hw] - 1;
+      const int t = hw * 16 + (bpos >> 2), j = bpos & 3;
       const int32_t s = score[(int64_t)row * Ns + 4 * (tid + BS * t) + j];
       const uint32_t tk = tk0 + (uint32_t)t * step + (uint32_t)j * m1;
       const int p = atomicAdd(&cnt, 1);
@@ -606,7 +611,7 @@ int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, in
   const int K = sp.n_cand;
   const int lim = c->select_lds_cap > 0 ? std::min(c->select_lds_cap, kSelLdsCap) : kSelLdsCap;
   const int cap = std::max(K + 1, lim);
-  const bool generic = c->select_generic || Ns > 4096 * 16;
+  const bool generic = c->select_generic || Ns > 3072 * 17;
   dim3 grid(rows);
 #define KP_SEL_T(V4, BS)                                                                 \
   hipLaunchKernelGGL((k_select_t<V4, BS>), grid, dim3(BS), 0, c->stream, sp, score, Ns,  \
@@ -634,8 +639,10 @@ int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, in
     KP_SEL_T(8, 256);
   } else if (Ns <= 1024 * 16) {
     KP_SEL_T(16, 256);
+  } else if (Ns <= 4096 * 8) {
+    KP_SEL_T(8, 1024);
   } else {
-    KP_SEL_T(16, 1024);
+    KP_SEL_T(17, 768);  // 12 waves (3 per SIMD, up to 168 VGPRs): no spill
   }
 #undef KP_SEL_T
   KP_HIP(hipGetLastError());

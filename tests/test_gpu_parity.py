@@ -397,3 +397,12 @@ def test_apply_delta_all_or_nothing(placer):
     placer.apply_delta(np.array([2, 2], np.int32), np.full((4, 2), 3, np.int64))
     after = placer.fetch()["used"]
     assert (after[:, 2] == before[:, 2] + 6).all()
+
+
+def test_place_widest_rows_parity(oracle, placer):
+    """Rows of 50k nodes (config #5's table) take the 768-thread select form."""
+    w = synth.config2(1_500, 50_000)
+    w.used = (w.cap * (np.arange(w.N) % 5) // 7).astype(np.int64)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[3])
+    g, o = _place_both(oracle, placer, w, p)
+    _assert_same(g, o, "widest rows")
