@@ -89,6 +89,8 @@ static int ensure_nodes(kp_ctx *c, int32_t N, int32_t D) {
   KP_TRY(dalloc(&c->d.seg_start, (size_t)n));
   KP_TRY(dalloc(&c->d.seg_end, (size_t)n));
   KP_TRY(dalloc(&c->d.roff, (size_t)n + 1));
+  KP_TRY(dalloc(&c->d.node_flag, (size_t)n));
+  KP_TRY(dalloc(&c->d.node_list, (size_t)n));
   c->cap_N = n;
   return KP_OK;
 }
@@ -315,7 +317,7 @@ void kp_destroy(kp_ctx *c) {
                   d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
                   d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.roff,
                   d.rreq, d.rsuf, d.rprio, d.pre_node, d.pre_vict, d.pre_cost,
-                  d.dl_node, d.dl_delta, d.dl_bad};
+                  d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->world > 1) {

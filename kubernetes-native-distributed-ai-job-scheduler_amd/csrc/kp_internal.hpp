@@ -77,6 +77,8 @@ struct DevState {
   int32_t *ent_slot = nullptr, *ent_size = nullptr, *ent_lead = nullptr;  // [U*K]
   int64_t *ent_q = nullptr;     // [D][U*K] request of the entry's unit
   int32_t *seg_start = nullptr, *seg_end = nullptr;  // [N]
+  int32_t *node_flag = nullptr; // [N] last pass in which the node received a bid
+  int32_t *node_list = nullptr; // [N] nodes with bidders this round (count: counters[32])
   int32_t *pass_flag = nullptr; // [64] pass p produced proposals
   // preemption: unit priorities, victim-pool CSR sorted
   // (node, prio desc, running index asc) with per-node suffix sums, outputs

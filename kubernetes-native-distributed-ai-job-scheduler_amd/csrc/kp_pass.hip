@@ -42,7 +42,8 @@ __global__ void k_csr_keys(int32_t A, int32_t K, int32_t N, int64_t nwin,
                            const int32_t *__restrict__ cand, uint32_t *__restrict__ keys,
                            uint32_t *__restrict__ vals, uint32_t *__restrict__ bid,
                            int32_t *__restrict__ win, int32_t *__restrict__ seg_start,
-                           int32_t *__restrict__ pass_flag) {
+                           int32_t *__restrict__ pass_flag, int32_t *__restrict__ node_flag,
+                           int32_t *__restrict__ nl_count) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < (int64_t)A * K) {
     const int32_t n = cand[t];
@@ -51,7 +52,11 @@ __global__ void k_csr_keys(int32_t A, int32_t K, int32_t N, int64_t nwin,
     vals[t] = ((uint32_t)a << 5) | (uint32_t)c;     // K <= 32
     bid[t] = kNoBid;
   }
-  if (t < N) seg_start[t] = -1;
+  if (t < N) {
+    seg_start[t] = -1;
+    node_flag[t] = -1;
+  }
+  if (t == 0) *nl_count = 0;
   if (t < nwin) win[t] = -1;
   if (t < 64) pass_flag[t] = 0;
 }
@@ -63,7 +68,8 @@ __global__ void k_csr_finish(int32_t P, int32_t N, int32_t K, int32_t D, int32_t
                              int32_t *__restrict__ seg_start, int32_t *__restrict__ seg_end,
                              int32_t *__restrict__ inv, int32_t *__restrict__ ent_unit,
                              int32_t *__restrict__ ent_slot, int32_t *__restrict__ ent_size,
-                             int32_t *__restrict__ ent_lead, int64_t *__restrict__ ent_q) {
+                             int32_t *__restrict__ ent_lead, int64_t *__restrict__ ent_q,
+                             int32_t *__restrict__ node_list, int32_t *__restrict__ nl_count) {
   int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= P) return;
   const uint32_t k = keys[e];
@@ -79,7 +85,10 @@ __global__ void k_csr_finish(int32_t P, int32_t N, int32_t K, int32_t D, int32_t
   ent_size[e] = size[u];
   ent_lead[e] = leader[u];
   for (int d = 0; d < D; ++d) ent_q[(int64_t)d * P + e] = q[(int64_t)d * U + u];
-  if (e == 0 || keys[e - 1] != k) seg_start[k] = e;
+  if (e == 0 || keys[e - 1] != k) {
+    seg_start[k] = e;
+    node_list[atomicAdd(nl_count, 1)] = (int32_t)k;  // any order: nodes are independent
+  }
   if (e == P - 1 || keys[e + 1] != k) seg_end[k] = e + 1;
 }
 
@@ -109,7 +118,8 @@ __global__ __launch_bounds__(256) void k_plan(ScoreParams sp, int32_t A, int32_t
                                               int32_t *__restrict__ pass_flag,
                                               int4 *__restrict__ gpart,
                                               int32_t *__restrict__ nparts,
-                                              int32_t *__restrict__ arrive) {
+                                              int32_t *__restrict__ arrive,
+                                              int32_t *__restrict__ node_flag) {
   constexpr int SPW = 64 / G;  // slots per wave
   constexpr uint64_t GMASK = G == 64 ? ~0ull : ((1ull << G) - 1);
   const int lane = threadIdx.x & 63;
@@ -191,6 +201,7 @@ __global__ __launch_bounds__(256) void k_plan(ScoreParams sp, int32_t A, int32_t
     bid[e_inv] = ((uint32_t)pass << 8) | (uint32_t)planned;
     s0_out[e_inv] = s0;
     win[e_inv >> 6] = pass;
+    node_flag[node] = pass;
     if (np > 1) {
       const int idx = __popcll(pm & ((1ull << gl) - 1));
       gpart[(int64_t)a * K + idx] = make_int4(node, planned, inc - planned, s0);
@@ -346,11 +357,21 @@ __global__ __launch_bounds__(256) void k_accept(ScoreParams sp, int32_t pass, in
                                                 const int32_t *__restrict__ ent_lead,
                                                 const int32_t *__restrict__ ent_slot,
                                                 const int64_t *__restrict__ cap,
-                                                AcceptOut o) {
+                                                const int32_t *__restrict__ node_flag,
+                                                const int32_t *__restrict__ node_list,
+                                                const int32_t *__restrict__ nl_count,
+                                                int32_t use_list, AcceptOut o) {
   const int lane = threadIdx.x & 63;
-  const int node = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int N = sp.N;
-  if (node >= N) return;
+  int node = wv;
+  if (use_list) {  // small rounds: one wave per node that has bidders this round
+    if (wv >= *nl_count) return;
+    node = node_list[wv];
+  } else if (node >= N) {
+    return;
+  }
+  const int32_t nf = node_flag[node];
   const int32_t e0 = seg_start[node];
   const int32_t e1 = seg_end[node];
   int64_t rem[D], add[D];
@@ -359,11 +380,12 @@ __global__ __launch_bounds__(256) void k_accept(ScoreParams sp, int32_t pass, in
     rem[d] = cap[(int64_t)d * N + node] - o.used[(int64_t)d * N + node];
     add[d] = 0;
   }
-  if (e0 < 0) return;
+  if (nf != pass || e0 < 0) return;  // nobody bid on this node in this pass
   const int32_t w0 = e0 >> 6, w1 = (e1 - 1) >> 6;
   constexpr int BATCH = 4;  // flagged windows whose operands are loaded together
   for (int wb = w0; wb <= w1; wb += 64) {
-    uint64_t flagged = __ballot(wb + lane <= w1 && win[wb + lane] == pass);
+    // a one-window segment is loaded without consulting its window flag
+    uint64_t flagged = w0 == w1 ? 1ull : __ballot(wb + lane <= w1 && win[wb + lane] == pass);
     while (flagged) {
       int wl[BATCH];
 #pragma unroll
@@ -402,14 +424,14 @@ struct PlanL {
                          sp, A, c->U, pass, c->d.act, c->d.cand, c->d.inv, c->d.open,
                          c->d.status, c->d.cap, c->d.used, c->d.R, c->d.base, c->d.topo, c->d.q,
                          c->d.size, c->d.bid, c->d.win, c->d.s0, c->d.pass_flag, c->d.gpart,
-                         c->d.nparts, c->d.arrive);
+                         c->d.nparts, c->d.arrive, c->d.node_flag);
     } else {
       constexpr int G = 32;
       hipLaunchKernelGGL((k_plan<D, G>), dim3(blocks(A, 4 * (64 / G))), dim3(256), 0, c->stream,
                          sp, A, c->U, pass, c->d.act, c->d.cand, c->d.inv, c->d.open,
                          c->d.status, c->d.cap, c->d.used, c->d.R, c->d.base, c->d.topo, c->d.q,
                          c->d.size, c->d.bid, c->d.win, c->d.s0, c->d.pass_flag, c->d.gpart,
-                         c->d.nparts, c->d.arrive);
+                         c->d.nparts, c->d.arrive, c->d.node_flag);
     }
     KP_HIP(hipGetLastError());
     return KP_OK;
@@ -432,9 +454,13 @@ struct AcceptL {
     o.status = c->d.status;
     o.job_node = c->d.job_node;
     o.job_score = c->d.job_score;
-    hipLaunchKernelGGL((k_accept<D>), dim3(blocks(c->N, 4)), dim3(256), 0, c->stream, sp, pass,
+    // rounds with fewer bidder entries than nodes walk the active-node list
+    const int32_t use_list = P < c->N ? 1 : 0;
+    const int64_t waves = use_list ? P : c->N;
+    hipLaunchKernelGGL((k_accept<D>), dim3(blocks(waves, 4)), dim3(256), 0, c->stream, sp, pass,
                        P, c->d.seg_start, c->d.seg_end, c->d.bid, c->d.win, c->d.s0, c->d.ent_q,
-                       c->d.ent_unit, c->d.ent_size, c->d.ent_lead, c->d.ent_slot, c->d.cap, o);
+                       c->d.ent_unit, c->d.ent_size, c->d.ent_lead, c->d.ent_slot, c->d.cap,
+                       c->d.node_flag, c->d.node_list, c->d.counters + 32, use_list, o);
     KP_HIP(hipGetLastError());
     return KP_OK;
   }
@@ -459,7 +485,7 @@ int launch_csr_build(kp_ctx *c, int32_t A, int32_t K) {
   const int64_t n = std::max<int64_t>(std::max<int64_t>(P, c->N), std::max<int64_t>(nwin, 64));
   hipLaunchKernelGGL(k_csr_keys, dim3(blocks(n, 256)), dim3(256), 0, c->stream, A, K, c->N, nwin,
                      c->d.cand, c->d.csr_kin, c->d.csr_vin, c->d.bid, c->d.win, c->d.seg_start,
-                     c->d.pass_flag);
+                     c->d.pass_flag, c->d.node_flag, c->d.counters + 32);
   KP_HIP(hipGetLastError());
   if (P == 0) return KP_OK;
   unsigned bits = 1;
@@ -470,7 +496,8 @@ int launch_csr_build(kp_ctx *c, int32_t A, int32_t K) {
   hipLaunchKernelGGL(k_csr_finish, dim3(blocks(P, 256)), dim3(256), 0, c->stream, (int32_t)P,
                      c->N, K, c->D, c->U, c->d.csr_keys, c->d.csr_vals, c->d.act, c->d.q,
                      c->d.size, c->d.leader, c->d.seg_start, c->d.seg_end, c->d.inv,
-                     c->d.ent_unit, c->d.ent_slot, c->d.ent_size, c->d.ent_lead, c->d.ent_q);
+                     c->d.ent_unit, c->d.ent_slot, c->d.ent_size, c->d.ent_lead, c->d.ent_q,
+                     c->d.node_list, c->d.counters + 32);
   KP_HIP(hipGetLastError());
   return KP_OK;
 }
