@@ -110,6 +110,8 @@ def main():
     ap.add_argument("--stream-batch", type=int, default=5_000)
     ap.add_argument("--stream-nodes", type=int, default=50_000)
     ap.add_argument("--no-stream", action="store_true")
+    ap.add_argument("--no-kernel-events", action="store_true",
+                    help="time the steps without per-launch HIP events (no roofline)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -140,7 +142,7 @@ def main():
     for _ in range(args.warmup):
         pl.reset_nodes()
         pl.solve(p)
-    pl.set_profiling(True)
+    pl.set_profiling(not args.no_kernel_events)
     barrier()
     t0 = time.perf_counter()
     score_ms = score_b = select_ms = 0.0

@@ -574,7 +574,10 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
       const int32_t rows = (int32_t)std::min<int64_t>(rpc, A_local - r0);
       EvPair e1, e2;
       if (c->profiling) KP_TRY(ev_begin(e1));
-      KP_TRY(launch_score(c, sp, c->d.act_local + r0, rows, c->d.score, c->d.mask, c->d.q, U));
+      // the solve needs only the score matrix: its -1 sentinel is the
+      // feasibility filter, so the bit mask (kp_score's second output) is
+      // not materialised here
+      KP_TRY(launch_score(c, sp, c->d.act_local + r0, rows, c->d.score, nullptr, c->d.q, U));
       if (c->profiling) {
         KP_HIP(hipEventRecord(e1.b, c->stream));
         kev.push_back({e1, 0});
@@ -587,8 +590,8 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
         kev.push_back({e2, 1});
       }
       tm.score_launches++;
-      tm.score_bytes += (int64_t)rows * Ns * 4 + (int64_t)rows * (Ns / 64) * 8 +
-                        (int64_t)8 * c->D * rows + (int64_t)3 * 8 * c->D * N + 8 * (int64_t)N;
+      tm.score_bytes += (int64_t)rows * Ns * 4 + (int64_t)8 * c->D * rows +
+                        (int64_t)3 * 8 * c->D * N + 8 * (int64_t)N;
       tm.select_bytes += (int64_t)rows * Ns * 4 + (int64_t)rows * K * 4;
     }
     if (c->world > 1) {

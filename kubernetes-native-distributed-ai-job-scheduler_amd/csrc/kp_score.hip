@@ -132,7 +132,7 @@ __device__ __forceinline__ uint32_t mul_u24(uint32_t a, uint32_t b) {
   return r;
 }
 
-template <int D>
+template <int D, bool MOST>
 __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
                                                  const int64_t *__restrict__ cap,
                                                  const int64_t *__restrict__ used,
@@ -144,18 +144,20 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
                                                  int32_t *__restrict__ score,
                                                  uint64_t *__restrict__ mask, int32_t Ns) {
   constexpr int NPL = 4;
-  __shared__ uint32_t sq[kScoreMaxRows][D];
+  __shared__ uint32_t sq[kScoreMaxRows][D + 1];  // [D] = request in the GPU dim (0 if none)
   const int N = sp.N;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int tile0 = blockIdx.x * 1024 + wave * 256;
   const int nb = tile0 + lane * NPL;  // first of this lane's 4 nodes
   const int r0 = blockIdx.y * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
-  if ((int)threadIdx.x < (r1 - r0) * D) {
-    const int rr = threadIdx.x / D, d = threadIdx.x % D;
-    sq[rr][d] = (uint32_t)q[(int64_t)d * qstride + rows_unit[r0 + rr]];
+  const int g = sp.gpu_dim;
+  if ((int)threadIdx.x < (r1 - r0) * (D + 1)) {
+    const int rr = threadIdx.x / (D + 1), d = threadIdx.x % (D + 1);
+    const int dd = d < D ? d : g;
+    sq[rr][d] = dd >= 0 ? (uint32_t)q[(int64_t)dd * qstride + rows_unit[r0 + rr]] : 0u;
   }
-  uint32_t f_[NPL][D], u_[NPL][D], rl_[NPL][D], rh_[NPL][D];
+  uint32_t f_[NPL][D], u_[NPL][D], rl_[NPL][D], rh_[NPL][D], fg_[NPL];
   int32_t b_[NPL];
   bool v_[NPL];
 #pragma unroll
@@ -163,6 +165,7 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
     const int n = nb + k;
     v_[k] = n < N;
     const int nn = v_[k] ? n : 0;
+    fg_[k] = 0xFFFFFFFFu;  // free GPUs: never equal to a request when there is no GPU dim
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       const int64_t cc = cap[(int64_t)d * N + nn], uu = used[(int64_t)d * N + nn];
@@ -171,46 +174,78 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
       u_[k][d] = (uint32_t)uu;
       rl_[k][d] = (uint32_t)rr;
       rh_[k][d] = (uint32_t)(rr >> 32);
+      if (d == g) fg_[k] = f_[k][d];
     }
     b_[k] = (int32_t)base[nn];
+  }
+  // wave-uniform: does any node of this wave need the Rh term in dim d?
+  // (Rh > 0 only where cap <= S; large-capacity dims skip the multiply)
+  bool need_rh[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    uint32_t any = 0;
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) any |= rh_[k][d];
+    need_rh[d] = __ballot(any != 0) != 0;
   }
   __syncthreads();
   if (tile0 >= Ns) return;  // wave-uniform, after the only barrier
   const int words = Ns >> 6;
   const bool store_ok = nb < Ns;  // Ns % 64 == 0: then all 4 nodes are in the row
+  const int32_t wfit = sp.w_gpu_fit;
   for (int r = r0; r < r1; ++r) {
     uint32_t qq[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) qq[d] = sq[r - r0][d];
-    int32_t sv[NPL];
-    uint64_t bal[NPL];
+    const uint32_t qg = sq[r - r0][D];
+    bool fits[NPL];
+    int32_t acc[NPL];
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
-      bool fits = v_[k];
-      int32_t acc = 0, fit_bonus = 0;
+      fits[k] = v_[k];
+      acc[k] = 0;
+    }
+    // dim-outer: one wave-uniform branch per dim for the Rh term
 #pragma unroll
-      for (int d = 0; d < D; ++d) {
-        fits &= qq[d] <= f_[k][d];
-        const uint32_t uu = u_[k][d] + qq[d];
-        // 24-bit multiplies (full rate) are exact wherever the pair fits:
-        // rh > 0 only if cap <= S <= 1024, and then uu <= cap; w <= 65535 and
-        // util <= S. Only mulhi stays a 32-bit (quarter-rate) multiply.
-        const uint32_t util = __umulhi(uu, rl_[k][d]) + mul_u24(uu, rh_[k][d]);
-        acc += (int32_t)__umul24((uint32_t)sp.w[d], util);
-        if (d == sp.gpu_dim && qq[d] > 0 && f_[k][d] == qq[d]) fit_bonus = sp.w_gpu_fit;
+    for (int d = 0; d < D; ++d) {
+      uint32_t uu[NPL], util[NPL];
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) {
+        fits[k] &= qq[d] <= f_[k][d];
+        uu[k] = u_[k][d] + qq[d];
+        util[k] = __umulhi(uu[k], rl_[k][d]);
       }
-      const int32_t s = (sp.most_allocated ? acc : b_[k] - acc) + fit_bonus;
-      sv[k] = fits ? s : KP_SCORE_INFEASIBLE;
-      bal[k] = __ballot(fits);
+      // 24-bit multiplies (full rate) are exact wherever the pair fits:
+      // rh > 0 only if cap <= S <= 1024, and then uu <= cap; w <= 65535 and
+      // util <= S. Only mulhi stays a 32-bit (quarter-rate) multiply.
+      if (need_rh[d]) {
+#pragma unroll
+        for (int k = 0; k < NPL; ++k) util[k] += mul_u24(uu[k], rh_[k][d]);
+      }
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) acc[k] += (int32_t)__umul24((uint32_t)sp.w[d], util[k]);
+    }
+    int32_t sv[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      // GPU-topology fit: the job takes exactly the node's free GPUs
+      const int32_t bonus = (qg != 0u && fg_[k] == qg) ? wfit : 0;
+      const int32_t s = (MOST ? acc[k] : b_[k] - acc[k]) + bonus;
+      sv[k] = fits[k] ? s : KP_SCORE_INFEASIBLE;
     }
     if (score && store_ok)
       *reinterpret_cast<int4 *>(score + (int64_t)r * Ns + nb) =
           make_int4(sv[0], sv[1], sv[2], sv[3]);
-    if (mask && lane < 4 && tile0 + 64 * lane < Ns) {
-      const int sh = 16 * lane;
-      const uint64_t wd = spread4_16(bal[0] >> sh) | (spread4_16(bal[1] >> sh) << 1) |
-                          (spread4_16(bal[2] >> sh) << 2) | (spread4_16(bal[3] >> sh) << 3);
-      mask[(int64_t)r * words + (tile0 >> 6) + lane] = wd;
+    if (mask) {  // wave-uniform: the solve passes no mask (the -1 sentinel is the filter)
+      uint64_t bal[NPL];
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) bal[k] = __ballot(fits[k]);
+      if (lane < 4 && tile0 + 64 * lane < Ns) {
+        const int sh = 16 * lane;
+        const uint64_t wd = spread4_16(bal[0] >> sh) | (spread4_16(bal[1] >> sh) << 1) |
+                            (spread4_16(bal[2] >> sh) << 2) | (spread4_16(bal[3] >> sh) << 3);
+        mask[(int64_t)r * words + (tile0 >> 6) + lane] = wd;
+      }
     }
   }
 }
@@ -568,8 +603,14 @@ struct ScoreL {
       const int64_t want = ((int64_t)rows * tiles + 2047) / 2048;
       const int rpb = (int)std::min<int64_t>(kScoreMaxRows, std::max<int64_t>(4, want));
       dim3 grid(tiles, blocks(rows, rpb));
-      hipLaunchKernelGGL((k_score32<D>), grid, dim3(256), 0, c->stream, sp, c->d.cap, c->d.used,
-                         c->d.R, c->d.base, q, qstride, rows_unit, rows, rpb, score, mask, Ns);
+      if (sp.most_allocated)
+        hipLaunchKernelGGL((k_score32<D, true>), grid, dim3(256), 0, c->stream, sp, c->d.cap,
+                           c->d.used, c->d.R, c->d.base, q, qstride, rows_unit, rows, rpb, score,
+                           mask, Ns);
+      else
+        hipLaunchKernelGGL((k_score32<D, false>), grid, dim3(256), 0, c->stream, sp, c->d.cap,
+                           c->d.used, c->d.R, c->d.base, q, qstride, rows_unit, rows, rpb, score,
+                           mask, Ns);
     } else {
       constexpr int NPL = D <= 4 ? 2 : 1;
       const int rpb = 32;
