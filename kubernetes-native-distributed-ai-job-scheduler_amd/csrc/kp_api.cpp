@@ -128,6 +128,7 @@ static int ensure_units(kp_ctx *c, int32_t U, int32_t J) {
     KP_TRY(dalloc(&c->d.csr_vals, pm));
     KP_TRY(dalloc(&c->d.pass_flag, 64));
     KP_TRY(dalloc(&c->d.counters, 64));
+    KP_TRY(dalloc(&c->d.stats, 1));
     c->d.temp_bytes = rocprim_temp_bytes((int32_t)std::min<size_t>(pm, INT32_MAX));
     KP_TRY(dalloc(reinterpret_cast<uint8_t **>(&c->d.temp), c->d.temp_bytes));
     if (c->world > 1) {
@@ -317,7 +318,7 @@ void kp_destroy(kp_ctx *c) {
                   d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
                   d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.roff,
                   d.rreq, d.rsuf, d.rprio, d.pre_node, d.pre_vict, d.pre_cost,
-                  d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list};
+                  d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.stats};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->world > 1) {
@@ -550,84 +551,128 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   hipEvent_t t0, t1;
   KP_HIP(hipEventCreate(&t0));
   KP_HIP(hipEventCreate(&t1));
+  KP_HIP(hipMemsetAsync(c->d.stats, 0, sizeof(SolveStats), c->stream));
+  KP_HIP(hipMemsetAsync(c->d.pass_flag, 0, sizeof(int32_t) * 64, c->stream));
   KP_HIP(hipEventRecord(t0, c->stream));
-  std::vector<std::pair<EvPair, int>> kev;  // (events, 0=score 1=select)
-  kp_timing tm{};
-  int64_t pairs = 0;
-  int32_t rounds = 0, passes = 0;
-  // pass flags of the previous round land in pinned memory; they are counted
-  // after the next stream synchronisation (no extra round trip per round)
-  int32_t *flags_h = c->pinned + 512;
-  bool flags_pending = false;
-  auto count_flags = [&]() {
-    if (!flags_pending) return;
-    for (int i = 0; i < p->max_passes; ++i) passes += flags_h[i] != 0;
-    flags_pending = false;
+  struct KEv {
+    EvPair e;
+    int kind;  // 0 = score, 1 = select
+    int32_t round;
+    int64_t rows_bound;
   };
-  while (true) {
-    if (p->max_rounds > 0 && rounds >= p->max_rounds) break;
-    int32_t A_local = 0, A = 0;
-    KP_TRY(launch_active(c, c->u_lo, c->u_hi, &A_local));
-    count_flags();
-    // candidates of this rank's active units: filter+score pass, then top-K select
-    for (int64_t r0 = 0; r0 < A_local; r0 += rpc) {
-      const int32_t rows = (int32_t)std::min<int64_t>(rpc, A_local - r0);
-      EvPair e1, e2;
-      if (c->profiling) KP_TRY(ev_begin(e1));
-      // the solve needs only the score matrix: its -1 sentinel is the
-      // feasibility filter, so the bit mask (kp_score's second output) is
-      // not materialised here
-      KP_TRY(launch_score(c, sp, c->d.act_local + r0, rows, c->d.score, nullptr, c->d.q, U));
-      if (c->profiling) {
-        KP_HIP(hipEventRecord(e1.b, c->stream));
-        kev.push_back({e1, 0});
-        KP_TRY(ev_begin(e2));
-      }
-      KP_TRY(launch_select(c, sp, c->d.act_local + r0, rows, c->d.score,
-                           c->d.cand_local + r0 * K));
-      if (c->profiling) {
-        KP_HIP(hipEventRecord(e2.b, c->stream));
-        kev.push_back({e2, 1});
-      }
-      tm.score_launches++;
-      tm.score_bytes += (int64_t)rows * Ns * 4 + (int64_t)8 * c->D * rows +
-                        (int64_t)3 * 8 * c->D * N + 8 * (int64_t)N;
-      tm.select_bytes += (int64_t)rows * Ns * 4 + (int64_t)rows * K * 4;
+  std::vector<KEv> kev;
+  std::vector<int32_t> round_active;  // exact active units per round (when known)
+  kp_timing tm{};
+  // filter+score and top-K select of `rows` rows starting at act_local[r0];
+  // rows_dev (nullable) clamps them to the device count
+  auto score_select = [&](int64_t r0, int32_t rows, const int32_t *rows_dev,
+                          int32_t round) -> int {
+    EvPair e1, e2;
+    if (c->profiling) KP_TRY(ev_begin(e1));
+    // the solve needs only the score matrix: its -1 sentinel is the
+    // feasibility filter, so the bit mask (kp_score's second output) is not
+    // materialised here
+    KP_TRY(launch_score(c, sp, c->d.act_local + r0, rows, c->d.score, nullptr, c->d.q, U,
+                        rows_dev));
+    if (c->profiling) {
+      KP_HIP(hipEventRecord(e1.b, c->stream));
+      kev.push_back({e1, 0, round, rows});
+      KP_TRY(ev_begin(e2));
     }
-    if (c->world > 1) {
-      KP_TRY(exchange_candidates(c, A_local, K, &A));
-    } else {
-      A = A_local;
+    KP_TRY(launch_select(c, sp, c->d.act_local + r0, rows, c->d.score, c->d.cand_local + r0 * K,
+                         rows_dev));
+    if (c->profiling) {
+      KP_HIP(hipEventRecord(e2.b, c->stream));
+      kev.push_back({e2, 1, round, rows});
     }
-    if (A == 0) break;
-    pairs += (int64_t)A * N;
-    KP_TRY(launch_open_init(c, A, K));
-    KP_TRY(launch_csr_build(c, A, K));  // also clears the round's pass flags
+    tm.score_launches++;
+    return KP_OK;
+  };
+  auto passes_of_round = [&](int32_t A, const int32_t *A_dev) -> int {
+    KP_TRY(launch_open_init(c, A, K, A_dev));
+    KP_TRY(launch_csr_build(c, A, K, A_dev));  // also banks + clears the pass flags
     // passes run back to back on the device: no host round trip inside a round
     for (int32_t pass = 0; pass < p->max_passes; ++pass) {
-      KP_TRY(launch_plan(c, sp, A, pass));
+      KP_TRY(launch_plan(c, sp, A, pass, A_dev));
       KP_TRY(launch_accept(c, sp, pass, A));
     }
-    KP_HIP(hipMemcpyAsync(flags_h, c->d.pass_flag, sizeof(int32_t) * 64, hipMemcpyDeviceToHost,
-                          c->stream));
-    flags_pending = true;
-    ++rounds;
+    return KP_OK;
+  };
+  if (c->world == 1) {
+    // Device-driven rounds: a round is enqueued with its grids sized by the
+    // previous round's active count (active units only shrink) and every
+    // kernel clamps to the device count. The host learns a round's count
+    // from an async copy that lands early in the round, while the GPU is
+    // still busy with it, so there is no idle gap between rounds. A round
+    // that turns out empty is a string of no-op launches and ends the solve.
+    hipEvent_t evA;
+    KP_HIP(hipEventCreateWithFlags(&evA, hipEventDisableTiming));
+    int32_t *A_h = c->pinned + 256;
+    int64_t A_bound = shard;
+    for (int32_t r = 0; A_bound > 0; ++r) {
+      if (p->max_rounds > 0 && r >= p->max_rounds) break;
+      KP_TRY(launch_active_async(c, c->u_lo, c->u_hi, A_h));
+      KP_HIP(hipEventRecord(evA, c->stream));
+      if (A_bound > rpc) {  // chunked score matrix: needs the exact count first
+        KP_HIP(hipEventSynchronize(evA));
+        const int32_t A = *A_h;
+        if (A == 0) break;
+        for (int64_t r0 = 0; r0 < A; r0 += rpc)
+          KP_TRY(score_select(r0, (int32_t)std::min<int64_t>(rpc, A - r0), nullptr, r));
+        round_active.push_back(A);
+        KP_TRY(passes_of_round(A, nullptr));
+        A_bound = A;
+        continue;
+      }
+      const int32_t *A_dev = c->d.counters;
+      KP_TRY(score_select(0, (int32_t)A_bound, A_dev, r));
+      KP_TRY(passes_of_round((int32_t)A_bound, A_dev));
+      KP_HIP(hipEventSynchronize(evA));  // landed long ago on a busy round
+      round_active.push_back(*A_h);
+      A_bound = *A_h;
+    }
+    (void)hipEventDestroy(evA);
+  } else {
+    // multi-GPU: the candidate exchange needs every rank's count on the host
+    for (int32_t r = 0;; ++r) {
+      if (p->max_rounds > 0 && r >= p->max_rounds) break;
+      int32_t A_local = 0, A = 0;
+      KP_TRY(launch_active(c, c->u_lo, c->u_hi, &A_local));
+      for (int64_t r0 = 0; r0 < A_local; r0 += rpc)
+        KP_TRY(score_select(r0, (int32_t)std::min<int64_t>(rpc, A_local - r0), nullptr, r));
+      round_active.push_back(A_local);
+      KP_TRY(exchange_candidates(c, A_local, K, &A));
+      if (A == 0) break;
+      KP_TRY(passes_of_round(A, nullptr));
+    }
   }
   KP_TRY(launch_finalize(c));
   KP_HIP(hipEventRecord(t1, c->stream));
-  // per-unit status for the stats
+  // per-unit status and the device-side statistics
   std::vector<int32_t> status(U);
   if (U > 0)
     KP_HIP(hipMemcpyAsync(status.data(), c->d.status, sizeof(int32_t) * U, hipMemcpyDeviceToHost,
                           c->stream));
+  SolveStats dst{};
+  KP_HIP(hipMemcpyAsync(&dst, c->d.stats, sizeof dst, hipMemcpyDeviceToHost, c->stream));
   KP_HIP(hipStreamSynchronize(c->stream));
-  count_flags();
+  const int32_t rounds = (int32_t)dst.rounds, passes = (int32_t)dst.passes;
+  const int64_t pairs = dst.active_sum * N;
   tm.solve_ms = ev_ms(t0, t1);
   for (auto &ke : kev) {
-    const double ms = ev_ms(ke.first.a, ke.first.b);
-    (ke.second == 0 ? tm.score_ms : tm.select_ms) += ms;
-    (void)hipEventDestroy(ke.first.a);
-    (void)hipEventDestroy(ke.first.b);
+    const double ms = ev_ms(ke.e.a, ke.e.b);
+    (ke.kind == 0 ? tm.score_ms : tm.select_ms) += ms;
+    // algorithmic bytes of the rows the launch actually had (device count)
+    int64_t rows = ke.rows_bound;
+    if (ke.round < (int32_t)round_active.size())
+      rows = std::min<int64_t>(rows, round_active[ke.round]);
+    if (ke.kind == 0)
+      tm.score_bytes += rows * Ns * 4 + (int64_t)8 * c->D * rows +
+                        (int64_t)3 * 8 * c->D * N + 8 * (int64_t)N;
+    else
+      tm.select_bytes += rows * Ns * 4 + rows * K * 4;
+    (void)hipEventDestroy(ke.e.a);
+    (void)hipEventDestroy(ke.e.b);
   }
   (void)hipEventDestroy(t0);
   (void)hipEventDestroy(t1);

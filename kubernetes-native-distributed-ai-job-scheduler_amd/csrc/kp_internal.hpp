@@ -26,6 +26,13 @@ static_assert(kTieMul * kTieMulInv == 1u, "tie multiplier must be invertible");
 
 enum UnitStatus : int32_t { kActive = 0, kPlaced = 1, kNoFit = 2 };
 
+// Solve statistics accumulated on the device (no per-round host round trip):
+// rounds with active units, sum of active units over rounds (x N = pairs
+// scored) and productive passes.
+struct SolveStats {
+  int64_t rounds, active_sum, passes, pad;
+};
+
 // Scoring constants copied into kernel arguments (wave-uniform -> SGPRs).
 struct ScoreParams {
   int32_t D;
@@ -94,6 +101,7 @@ struct DevState {
   int64_t *dl_delta = nullptr;  // [D][K]
   int32_t *dl_bad = nullptr;    // [16] violation flag (allocated at kp_create)
   int32_t *counters = nullptr;  // small device counters
+  SolveStats *stats = nullptr;  // [1]
   void *temp = nullptr;         // rocprim temporary storage
   size_t temp_bytes = 0;
   // dist exchange
@@ -144,14 +152,20 @@ struct kp_ctx {
 // Kernel launchers (kp_score.hip, kp_pass.hip).
 namespace kp {
 int launch_prep_nodes(kp_ctx *c, int32_t S, int most_allocated, const int32_t *w);
+// Kernels that take a device count pointer (rows_dev / A_dev, nullable) size
+// their grid by the host bound and clamp to the device count, so a round can
+// be enqueued before the host knows its exact number of active units.
 int launch_score(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit,
                  int32_t rows, int32_t *score, uint64_t *mask, const int64_t *q,
-                 int32_t qstride);
+                 int32_t qstride, const int32_t *rows_dev = nullptr);
 int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit,
-                  int32_t rows, const int32_t *score, int32_t *cand);
-int launch_open_init(kp_ctx *c, int32_t A, int32_t K);
-int launch_csr_build(kp_ctx *c, int32_t A, int32_t K);
-int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass);
+                  int32_t rows, const int32_t *score, int32_t *cand,
+                  const int32_t *rows_dev = nullptr);
+int launch_open_init(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev = nullptr);
+int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev = nullptr);
+int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass,
+                const int32_t *A_dev = nullptr);
+int launch_active_async(kp_ctx *c, int32_t lo, int32_t hi, int32_t *count_host);
 int launch_accept(kp_ctx *c, const ScoreParams &sp, int32_t pass, int32_t A);
 int launch_active(kp_ctx *c, int32_t lo, int32_t hi, int32_t *A_host);
 int launch_reset_units(kp_ctx *c);

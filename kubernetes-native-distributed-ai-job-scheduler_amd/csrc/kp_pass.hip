@@ -43,10 +43,12 @@ __global__ void k_csr_keys(int32_t A, int32_t K, int32_t N, int64_t nwin,
                            uint32_t *__restrict__ vals, uint32_t *__restrict__ bid,
                            int32_t *__restrict__ win, int32_t *__restrict__ seg_start,
                            int32_t *__restrict__ pass_flag, int32_t *__restrict__ node_flag,
-                           int32_t *__restrict__ nl_count) {
+                           int32_t *__restrict__ nl_count, const int32_t *__restrict__ A_dev,
+                           SolveStats *__restrict__ st) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int32_t Aa = A_dev ? min(A, *A_dev) : A;  // slots past the device count: no bids
   if (t < (int64_t)A * K) {
-    const int32_t n = cand[t];
+    const int32_t n = t < (int64_t)Aa * K ? cand[t] : -1;
     const int32_t a = (int32_t)(t / K), c = (int32_t)(t % K);
     keys[t] = n >= 0 ? (uint32_t)n : (uint32_t)N;  // invalid entries sort after every node
     vals[t] = ((uint32_t)a << 5) | (uint32_t)c;     // K <= 32
@@ -58,7 +60,10 @@ __global__ void k_csr_keys(int32_t A, int32_t K, int32_t N, int64_t nwin,
   }
   if (t == 0) *nl_count = 0;
   if (t < nwin) win[t] = -1;
-  if (t < 64) pass_flag[t] = 0;
+  if (t < 64) {  // the previous round's productive passes, then clear
+    if (pass_flag[t] != 0) atomicAdd(reinterpret_cast<unsigned long long *>(&st->passes), 1ull);
+    pass_flag[t] = 0;
+  }
 }
 
 __global__ void k_csr_finish(int32_t P, int32_t N, int32_t K, int32_t D, int32_t U,
@@ -99,7 +104,8 @@ __global__ void k_csr_finish(int32_t P, int32_t N, int32_t K, int32_t D, int32_t
 // (max value, lowest lane). All first-level loads (slot state, unit, candidate,
 // entry index) are issued together, before the open test.
 template <int D, int G>
-__global__ __launch_bounds__(256) void k_plan(ScoreParams sp, int32_t A, int32_t U, int32_t pass,
+__global__ __launch_bounds__(256) void k_plan(ScoreParams sp, int32_t A, const int32_t *__restrict__ A_dev,
+                                              int32_t U, int32_t pass,
                                               const int32_t *__restrict__ act,
                                               const int32_t *__restrict__ cand,
                                               const int32_t *__restrict__ inv,
@@ -128,6 +134,7 @@ __global__ __launch_bounds__(256) void k_plan(ScoreParams sp, int32_t A, int32_t
   const int wave_global = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int a = wave_global * SPW + lane / G;
   const int K = sp.n_cand, N = sp.N;
+  if (A_dev) A = min(A, *A_dev);
   const bool in = a < A;
   const int aa = in ? a : 0;  // A > 0: slot 0 exists
   const uint8_t op = open[aa];
@@ -417,18 +424,19 @@ __global__ __launch_bounds__(256) void k_accept(ScoreParams sp, int32_t pass, in
 
 template <int D>
 struct PlanL {
-  static int run(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass) {
+  static int run(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass,
+                 const int32_t *A_dev) {
     if (sp.n_cand <= 16) {
       constexpr int G = 16;
       hipLaunchKernelGGL((k_plan<D, G>), dim3(blocks(A, 4 * (64 / G))), dim3(256), 0, c->stream,
-                         sp, A, c->U, pass, c->d.act, c->d.cand, c->d.inv, c->d.open,
+                         sp, A, A_dev, c->U, pass, c->d.act, c->d.cand, c->d.inv, c->d.open,
                          c->d.status, c->d.cap, c->d.used, c->d.R, c->d.base, c->d.topo, c->d.q,
                          c->d.size, c->d.bid, c->d.win, c->d.s0, c->d.pass_flag, c->d.gpart,
                          c->d.nparts, c->d.arrive, c->d.node_flag);
     } else {
       constexpr int G = 32;
       hipLaunchKernelGGL((k_plan<D, G>), dim3(blocks(A, 4 * (64 / G))), dim3(256), 0, c->stream,
-                         sp, A, c->U, pass, c->d.act, c->d.cand, c->d.inv, c->d.open,
+                         sp, A, A_dev, c->U, pass, c->d.act, c->d.cand, c->d.inv, c->d.open,
                          c->d.status, c->d.cap, c->d.used, c->d.R, c->d.base, c->d.topo, c->d.q,
                          c->d.size, c->d.bid, c->d.win, c->d.s0, c->d.pass_flag, c->d.gpart,
                          c->d.nparts, c->d.arrive, c->d.node_flag);
@@ -479,13 +487,13 @@ size_t rocprim_temp_bytes(int32_t max_items) {
 }
 
 // node -> bidder inverse index of this round's candidates (one sort per round)
-int launch_csr_build(kp_ctx *c, int32_t A, int32_t K) {
+int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev) {
   const int64_t P = (int64_t)A * K;
   const int64_t nwin = (P + 63) / 64 + 64;
   const int64_t n = std::max<int64_t>(std::max<int64_t>(P, c->N), std::max<int64_t>(nwin, 64));
   hipLaunchKernelGGL(k_csr_keys, dim3(blocks(n, 256)), dim3(256), 0, c->stream, A, K, c->N, nwin,
                      c->d.cand, c->d.csr_kin, c->d.csr_vin, c->d.bid, c->d.win, c->d.seg_start,
-                     c->d.pass_flag, c->d.node_flag, c->d.counters + 32);
+                     c->d.pass_flag, c->d.node_flag, c->d.counters + 32, A_dev, c->d.stats);
   KP_HIP(hipGetLastError());
   if (P == 0) return KP_OK;
   unsigned bits = 1;
@@ -502,9 +510,9 @@ int launch_csr_build(kp_ctx *c, int32_t A, int32_t K) {
   return KP_OK;
 }
 
-int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass) {
+int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass, const int32_t *A_dev) {
   if (A <= 0) return KP_OK;
-  return dispatch_D<PlanL>(c->D, c, sp, A, pass);
+  return dispatch_D<PlanL>(c->D, c, sp, A, pass, A_dev);
 }
 
 int launch_accept(kp_ctx *c, const ScoreParams &sp, int32_t pass, int32_t A) {

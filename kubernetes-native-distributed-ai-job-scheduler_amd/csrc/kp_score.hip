@@ -56,7 +56,10 @@ __global__ __launch_bounds__(256) void k_score(ScoreParams sp,
                                                const int32_t *__restrict__ rows_unit,
                                                int32_t rows, int32_t rows_per_block,
                                                int32_t *__restrict__ score,
-                                               uint64_t *__restrict__ mask, int32_t Ns) {
+                                               uint64_t *__restrict__ mask, int32_t Ns,
+                                               const int32_t *__restrict__ rows_dev) {
+  if (rows_dev) rows = min(rows, *rows_dev);
+  if ((int)blockIdx.y * rows_per_block >= rows) return;  // block-uniform
   const int N = sp.N;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int tile0 = blockIdx.x * (256 * NPL) + wave * (64 * NPL);
@@ -142,8 +145,11 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
                                                  const int32_t *__restrict__ rows_unit,
                                                  int32_t rows, int32_t rows_per_block,
                                                  int32_t *__restrict__ score,
-                                                 uint64_t *__restrict__ mask, int32_t Ns) {
+                                                 uint64_t *__restrict__ mask, int32_t Ns,
+                                                 const int32_t *__restrict__ rows_dev) {
   constexpr int NPL = 4;
+  if (rows_dev) rows = min(rows, *rows_dev);
+  if ((int)blockIdx.y * rows_per_block >= rows) return;  // block-uniform
   __shared__ uint32_t sq[kScoreMaxRows][D + 1];  // [D] = request in the GPU dim (0 if none)
   const int N = sp.N;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -287,7 +293,8 @@ __global__ __launch_bounds__(BS) void k_select_t(ScoreParams sp,
                                                  const int32_t *__restrict__ score, int32_t Ns,
                                                  const int32_t *__restrict__ rows_unit,
                                                  const uint32_t *__restrict__ salt, int32_t rows,
-                                                 int32_t lds_cap, int32_t *__restrict__ cand) {
+                                                 int32_t lds_cap, int32_t *__restrict__ cand,
+                                                 const int32_t *__restrict__ rows_dev) {
   constexpr int NW = BS / 64;
   __shared__ uint64_t buf[kSelLdsCap];
   __shared__ uint64_t wth[NW];
@@ -295,7 +302,7 @@ __global__ __launch_bounds__(BS) void k_select_t(ScoreParams sp,
   __shared__ int cnt;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int row = blockIdx.x;
-  if (row >= rows) return;  // block-uniform
+  if (row >= rows || (rows_dev && row >= *rows_dev)) return;  // block-uniform
   const int K = sp.n_cand;
   const int32_t unit = rows_unit[row];
   const uint32_t sl = sp.tie_rotated ? salt[unit] : 0u;
@@ -429,11 +436,12 @@ __global__ __launch_bounds__(256) void k_select(ScoreParams sp,
                                                 const int32_t *__restrict__ score, int32_t Ns,
                                                 const int32_t *__restrict__ rows_unit,
                                                 const uint32_t *__restrict__ salt,
-                                                int32_t rows, int32_t *__restrict__ cand) {
+                                                int32_t rows, int32_t *__restrict__ cand,
+                                                const int32_t *__restrict__ rows_dev) {
   __shared__ uint64_t part[4][KC];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int row = blockIdx.x;
-  if (row >= rows) return;  // block-uniform
+  if (row >= rows || (rows_dev && row >= *rows_dev)) return;  // block-uniform
   const int K = sp.n_cand;
   const int32_t unit = rows_unit[row];
   const uint32_t sl = sp.tie_rotated ? salt[unit] : 0u;
@@ -498,8 +506,14 @@ __global__ __launch_bounds__(256) void k_select(ScoreParams sp,
 // ---------------------------------------------------------------------------
 __global__ void k_open_init(const int32_t *__restrict__ act, const int32_t *__restrict__ cand,
                             int32_t A, int32_t K, uint8_t *__restrict__ open,
-                            int32_t *__restrict__ status) {
+                            int32_t *__restrict__ status, const int32_t *__restrict__ A_dev,
+                            SolveStats *__restrict__ st) {
+  if (A_dev) A = min(A, *A_dev);
   int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a == 0 && A > 0) {  // one writer: a round with active units
+    st->rounds += 1;
+    st->active_sum += A;
+  }
   if (a >= A) return;
   const bool has = cand[(int64_t)a * K] >= 0;
   open[a] = has ? 1 : 0;
@@ -526,8 +540,13 @@ __global__ void k_flag_active(const int32_t *__restrict__ status, int32_t lo, in
 __global__ void k_finalize(const int32_t *__restrict__ status, const int32_t *__restrict__ leader,
                            const int32_t *__restrict__ size, int32_t U,
                            int32_t *__restrict__ job_node, int32_t *__restrict__ job_score,
-                           int32_t *__restrict__ job_status) {
+                           int32_t *__restrict__ job_status, const int32_t *__restrict__ pass_flag,
+                           SolveStats *__restrict__ stats) {
   int u = blockIdx.x * blockDim.x + threadIdx.x;
+  // the last round's productive passes (earlier rounds are counted when the
+  // next round's index build clears the flags)
+  if (u < 64 && pass_flag[u] != 0)
+    atomicAdd(reinterpret_cast<unsigned long long *>(&stats->passes), 1ull);
   if (u >= U) return;
   const int32_t st = status[u];
   const int32_t code = st == kPlaced ? KP_JOB_PLACED : st == kNoFit ? KP_JOB_NO_FIT
@@ -594,7 +613,8 @@ __global__ void k_delta_check(int32_t K, int32_t N, int32_t D, const int32_t *__
 template <int D>
 struct ScoreL {
   static int run(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
-                 int32_t *score, uint64_t *mask, const int64_t *q, int32_t qstride) {
+                 int32_t *score, uint64_t *mask, const int64_t *q, int32_t qstride,
+                 const int32_t *rows_dev) {
     const int Ns = (c->N + 63) & ~63;
     if (c->fits32) {
       // rows per workgroup: enough workgroups to cover the 256 CUs several
@@ -606,18 +626,18 @@ struct ScoreL {
       if (sp.most_allocated)
         hipLaunchKernelGGL((k_score32<D, true>), grid, dim3(256), 0, c->stream, sp, c->d.cap,
                            c->d.used, c->d.R, c->d.base, q, qstride, rows_unit, rows, rpb, score,
-                           mask, Ns);
+                           mask, Ns, rows_dev);
       else
         hipLaunchKernelGGL((k_score32<D, false>), grid, dim3(256), 0, c->stream, sp, c->d.cap,
                            c->d.used, c->d.R, c->d.base, q, qstride, rows_unit, rows, rpb, score,
-                           mask, Ns);
+                           mask, Ns, rows_dev);
     } else {
       constexpr int NPL = D <= 4 ? 2 : 1;
       const int rpb = 32;
       dim3 grid(blocks(Ns, 256 * NPL), blocks(rows, rpb));
       hipLaunchKernelGGL((k_score<D, NPL>), grid, dim3(256), 0, c->stream, sp, c->d.cap,
                          c->d.used, c->d.R, c->d.base, q, qstride, rows_unit, rows, rpb, score,
-                         mask, Ns);
+                         mask, Ns, rows_dev);
     }
     KP_HIP(hipGetLastError());
     return KP_OK;
@@ -640,13 +660,14 @@ int launch_prep_nodes(kp_ctx *c, int32_t S, int most_allocated, const int32_t *w
 }
 
 int launch_score(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
-                 int32_t *score, uint64_t *mask, const int64_t *q, int32_t qstride) {
+                 int32_t *score, uint64_t *mask, const int64_t *q, int32_t qstride,
+                 const int32_t *rows_dev) {
   if (rows <= 0 || c->N == 0) return KP_OK;
-  return dispatch_D<ScoreL>(c->D, c, sp, rows_unit, rows, score, mask, q, qstride);
+  return dispatch_D<ScoreL>(c->D, c, sp, rows_unit, rows, score, mask, q, qstride, rows_dev);
 }
 
 int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
-                  const int32_t *score, int32_t *cand) {
+                  const int32_t *score, int32_t *cand, const int32_t *rows_dev) {
   if (rows <= 0) return KP_OK;
   const int Ns = (c->N + 63) & ~63;
   const int K = sp.n_cand;
@@ -656,20 +677,20 @@ int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, in
   dim3 grid(rows);
 #define KP_SEL_T(V4, BS)                                                                 \
   hipLaunchKernelGGL((k_select_t<V4, BS>), grid, dim3(BS), 0, c->stream, sp, score, Ns,  \
-                     rows_unit, c->d.salt, rows, cap, cand)
+                     rows_unit, c->d.salt, rows, cap, cand, rows_dev)
   if (generic) {
     if (K <= 4)
       hipLaunchKernelGGL(k_select<4>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
-                         c->d.salt, rows, cand);
+                         c->d.salt, rows, cand, rows_dev);
     else if (K <= 8)
       hipLaunchKernelGGL(k_select<8>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
-                         c->d.salt, rows, cand);
+                         c->d.salt, rows, cand, rows_dev);
     else if (K <= 16)
       hipLaunchKernelGGL(k_select<16>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
-                         c->d.salt, rows, cand);
+                         c->d.salt, rows, cand, rows_dev);
     else
       hipLaunchKernelGGL(k_select<32>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
-                         c->d.salt, rows, cand);
+                         c->d.salt, rows, cand, rows_dev);
   } else if (Ns <= 1024 * 1) {
     KP_SEL_T(1, 256);
   } else if (Ns <= 1024 * 2) {
@@ -690,10 +711,10 @@ int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, in
   return KP_OK;
 }
 
-int launch_open_init(kp_ctx *c, int32_t A, int32_t K) {
+int launch_open_init(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev) {
   if (A <= 0) return KP_OK;
   hipLaunchKernelGGL(k_open_init, dim3(blocks(A, 256)), dim3(256), 0, c->stream, c->d.act,
-                     c->d.cand, A, K, c->d.open, c->d.status);
+                     c->d.cand, A, K, c->d.open, c->d.status, A_dev, c->d.stats);
   KP_HIP(hipGetLastError());
   return KP_OK;
 }
@@ -739,6 +760,23 @@ int launch_delta(kp_ctx *c, int32_t K, int32_t *bad_host) {
   return KP_OK;
 }
 
+// same compaction without the host round trip: the count stays on the device
+// (counters[0], read by the round's kernels) and is copied to *count_host
+// asynchronously
+int launch_active_async(kp_ctx *c, int32_t lo, int32_t hi, int32_t *count_host) {
+  const int32_t n = hi - lo;
+  if (n <= 0) return KP_EINVAL;
+  hipLaunchKernelGGL(k_flag_active, dim3(blocks(n, 256)), dim3(256), 0, c->stream, c->d.status,
+                     lo, hi, c->d.flag);
+  KP_HIP(hipGetLastError());
+  size_t tb = c->d.temp_bytes;
+  KP_HIP(rocprim::select(c->d.temp, tb, rocprim::counting_iterator<int32_t>(lo), c->d.flag,
+                         c->d.act_local, c->d.counters, (size_t)n, c->stream));
+  KP_HIP(hipMemcpyAsync(count_host, c->d.counters, sizeof(int32_t), hipMemcpyDeviceToHost,
+                        c->stream));
+  return KP_OK;
+}
+
 int launch_reset_units(kp_ctx *c) {
   const int32_t n = c->U > c->J ? c->U : c->J;
   if (n <= 0) return KP_OK;
@@ -749,10 +787,10 @@ int launch_reset_units(kp_ctx *c) {
 }
 
 int launch_finalize(kp_ctx *c) {
-  if (c->U <= 0) return KP_OK;
-  hipLaunchKernelGGL(k_finalize, dim3(blocks(c->U, 256)), dim3(256), 0, c->stream, c->d.status,
+  const int32_t n = std::max(c->U, 64);
+  hipLaunchKernelGGL(k_finalize, dim3(blocks(n, 256)), dim3(256), 0, c->stream, c->d.status,
                      c->d.leader, c->d.size, c->U, c->d.job_node, c->d.job_score,
-                     c->d.job_status);
+                     c->d.job_status, c->d.pass_flag, c->d.stats);
   KP_HIP(hipGetLastError());
   return KP_OK;
 }
