@@ -39,25 +39,81 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
   }
   return v;
 }
-// max over aligned groups of G lanes (G a power of two <= 64)
-template <int G>
-__device__ __forceinline__ int64_t group_max_i64(int64_t v) {
-#pragma unroll
-  for (int m = G / 2; m >= 1; m >>= 1) {
-    int64_t o = (int64_t)shfl_xor_u64((uint64_t)v, m);
-    v = o > v ? o : v;
-  }
+// DPP lane move of a 64-bit value (two 32-bit v_mov_dpp); lanes whose
+// source is outside the pattern get an unspecified value and must not use it
+template <int CTRL>
+__device__ __forceinline__ int64_t dpp_i64(int64_t v) {
+  const int lo = (int)(uint32_t)(uint64_t)v, hi = (int)(uint32_t)((uint64_t)v >> 32);
+  const uint32_t l2 = (uint32_t)__builtin_amdgcn_mov_dpp(lo, CTRL, 0xf, 0xf, false);
+  const uint32_t h2 = (uint32_t)__builtin_amdgcn_mov_dpp(hi, CTRL, 0xf, 0xf, false);
+  return (int64_t)(((uint64_t)h2 << 32) | l2);
+}
+// inclusive prefix sum over the 64 lanes with DPP (row_shr 1/2/4/8 inside
+// each 16-lane row, then row_bcast 15/31 across rows): VALU-only, no LDS
+// crossbar round trips
+__device__ __forceinline__ int64_t wave_incl_scan_i64(int64_t v) {
+  const int l = lane_id(), rl = l & 15;
+  int64_t t;
+  t = dpp_i64<0x111>(v);
+  if (rl >= 1) v += t;
+  t = dpp_i64<0x112>(v);
+  if (rl >= 2) v += t;
+  t = dpp_i64<0x114>(v);
+  if (rl >= 4) v += t;
+  t = dpp_i64<0x118>(v);
+  if (rl >= 8) v += t;
+  t = dpp_i64<0x142>(v);  // row_bcast:15
+  if ((l & 31) >= 16) v += t;
+  t = dpp_i64<0x143>(v);  // row_bcast:31
+  if (l >= 32) v += t;
   return v;
 }
-// inclusive prefix sum over the 64 lanes (Hillis-Steele, 6 steps)
-__device__ __forceinline__ int64_t wave_incl_scan_i64(int64_t v) {
-  const int l = lane_id();
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    int64_t o = shfl_up_i64(v, d);
-    if (l >= d) v += o;
+// max over aligned groups of G lanes (G = 16, 32 or 64), result in every
+// lane of the group: DPP max-scan inside the group, then the group's last
+// lane is read back with scalar readlanes (no LDS crossbar)
+template <int G>
+__device__ __forceinline__ int64_t group_max_i64(int64_t v);
+
+// value of a wave-uniform lane (scalar read, no LDS)
+__device__ __forceinline__ int64_t readlane_i64(int64_t v, int lane) {
+  const int ln = __builtin_amdgcn_readfirstlane(lane);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, ln);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), ln);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+template <int G>
+__device__ __forceinline__ int64_t group_max_i64(int64_t v) {
+  static_assert(G == 16 || G == 32 || G == 64, "group size");
+  const int l = lane_id(), rl = l & 15;
+  int64_t t;
+  t = dpp_i64<0x111>(v);
+  if (rl >= 1) v = t > v ? t : v;
+  t = dpp_i64<0x112>(v);
+  if (rl >= 2) v = t > v ? t : v;
+  t = dpp_i64<0x114>(v);
+  if (rl >= 4) v = t > v ? t : v;
+  t = dpp_i64<0x118>(v);
+  if (rl >= 8) v = t > v ? t : v;
+  if (G >= 32) {
+    t = dpp_i64<0x142>(v);  // row_bcast:15
+    if ((l & 31) >= 16) v = t > v ? t : v;
   }
-  return v;
+  if (G >= 64) {
+    t = dpp_i64<0x143>(v);  // row_bcast:31
+    if (l >= 32) v = t > v ? t : v;
+  }
+  if (G == 16) {
+    const int64_t m0 = readlane_i64(v, 15), m1 = readlane_i64(v, 31);
+    const int64_t m2 = readlane_i64(v, 47), m3 = readlane_i64(v, 63);
+    const int g = l >> 4;
+    return g == 0 ? m0 : g == 1 ? m1 : g == 2 ? m2 : m3;
+  }
+  if (G == 32) {
+    const int64_t m0 = readlane_i64(v, 31), m1 = readlane_i64(v, 63);
+    return l < 32 ? m0 : m1;
+  }
+  return readlane_i64(v, 63);
 }
 
 // §2.3: score of one more copy of q on a node whose usage is `used`;

@@ -325,13 +325,13 @@ __device__ __forceinline__ void decide_window(const Win<D> &wc, int64_t (&rem)[D
     if (failm == 0) {
       accepted |= fa;
 #pragma unroll
-      for (int d = 0; d < D; ++d) rem[d] -= shfl_i64(pre[d], 63) + shfl_i64(fa ? wc.need[d] : 0, 63);
+      for (int d = 0; d < D; ++d) rem[d] -= readlane_i64(pre[d] + (fa ? wc.need[d] : 0), 63);
       break;
     }
     const int f = __ffsll((unsigned long long)failm) - 1;
     accepted |= fa && lane < f;
 #pragma unroll
-    for (int d = 0; d < D; ++d) rem[d] -= shfl_i64(pre[d], f);
+    for (int d = 0; d < D; ++d) rem[d] -= readlane_i64(pre[d], f);
     undecided = fa && lane >= f;  // lane f is rejected on the next check
   }
   if (wc.m > 0 && accepted) {
@@ -415,7 +415,7 @@ __global__ __launch_bounds__(256) void k_accept(ScoreParams sp, int32_t pass, in
   // fold the single-node units committed by this wave into `used`
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    const int64_t tot = wave_incl_scan_i64(add[d]);
+    const int64_t tot = readlane_i64(wave_incl_scan_i64(add[d]), 63);
     if (lane == 63 && tot != 0)
       atomicAdd(reinterpret_cast<unsigned long long *>(&o.used[(int64_t)d * N + node]),
                 (unsigned long long)tot);
