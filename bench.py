@@ -169,6 +169,14 @@ def main():
         return
     pairs = float(args.jobs) * args.nodes
     achieved = (score_b / 1e9) / (score_ms / 1e3) if score_ms > 0 else 0.0
+    traffic, traffic_src = None, None
+    pmc = os.path.join(REPO, "profiles", "r01_pmc.json")
+    if os.path.exists(pmc):  # HBM-side bytes per launch from rocprofv3 PMC passes
+        with open(pmc) as f:
+            k = [v for n, v in json.load(f)["kernels"].items() if n.startswith("k_score")]
+        if k:
+            traffic = k[0]["traffic_bytes_per_launch"]
+            traffic_src = "profiles/r01_pmc.json (FETCH_SIZE x2 + WRITE_SIZE, tools/gpu_pmc.sh)"
     out = {
         "metric": METRIC,
         "value": pairs / (ms / 1e3),
@@ -191,7 +199,10 @@ def main():
         "latency_ms": ms,
         "roofline": {"bound": "hbm", "kernel": "k_score (filter+score, materialised matrix)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": score_b / max(launches, 1),
+                     "frac_of_achievable_6290": achieved / 6290.0,
                      "launches_per_step": launches / args.steps,
                      "avg_launch_ms": score_ms / max(launches, 1)},
     }
