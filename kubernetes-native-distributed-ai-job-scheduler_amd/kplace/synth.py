@@ -202,10 +202,47 @@ def config5_completions(batch_no: int, running_jobs: np.ndarray) -> np.ndarray:
     return (x % np.uint64(5)) == np.uint64(0)
 
 
+def config1_objects(sample_specs: list[dict], K: int = 100, N: int = 64):
+    """#1: the reference's sample CRs (config/samples, as committed in
+    tests/golden/sample_crs.json) plus K synthetic LLMService CRs
+    (replicas in [1,8], gpuPerReplica in {0,1,2,4,8}, gpuMemory "<n>Gi") and N
+    synthetic corev1.Node reports (shapes A-D, topology label = n // 32), as
+    API-object dicts for the snapshot packer (kplace/packer.py)."""
+    seed = SEED_BASE + 1
+    crs = []
+    for i, spec in enumerate(sample_specs):
+        crs.append({"metadata": {"name": f"sample-{i}", "namespace": "default"},
+                    "spec": dict(spec)})
+    r = [splitmix64(seed, 1, np.arange(K, dtype=np.uint64) * np.uint64(4) + np.uint64(k))
+         for k in range(4)]
+    reps = draw(r[0], 1, 8)
+    gpu = np.array([0, 1, 2, 4, 8], np.int64)[(r[1] % np.uint64(5)).astype(np.int64)]
+    gmem = draw(r[2], 2, 48) * np.maximum(gpu, 1)
+    prio = draw(r[3], 0, 3)
+    for k in range(K):
+        crs.append({"metadata": {"name": f"llm-{k}", "namespace": "default",
+                                 "annotations": {"kubeinfer.ai/priority": str(int(prio[k]))}},
+                    "spec": {"model": f"org/model-{k % 7}", "replicas": int(reps[k]),
+                             "gpuPerReplica": int(gpu[k]), "gpuMemory": f"{int(gmem[k])}Gi"}})
+    x = splitmix64(seed, 0, np.arange(N, dtype=np.uint64))
+    shape = (x % np.uint64(4)).astype(np.int64)
+    nodes = []
+    for n in range(N):
+        cpu, mem, g, gm = (int(v) for v in SHAPES[shape[n]])
+        labels = {"kubeinfer.ai/xgmi-island": f"island-{n // 32}"}
+        if g:
+            labels["kubeinfer.ai/gpu-memory"] = f"{gm // g // 1024}Gi"
+        nodes.append({"metadata": {"name": f"node-{n:03d}", "labels": labels},
+                      "status": {"allocatable": {"cpu": str(cpu // 1000), "memory": f"{mem}Mi",
+                                                 "amd.com/gpu": str(g)}}})
+    return crs, nodes
+
+
 # scoring knobs per config (DESIGN.md §2.7)
 CONFIG_PARAMS = {
     2: dict(w_dim=(1, 1, 1, 1), w_gpu_fit=0, w_spread=0),
     3: dict(w_dim=(1, 1, 4, 2), w_gpu_fit=1024, w_spread=256),
+    1: dict(w_dim=(1, 1, 4, 2), w_gpu_fit=1024, w_spread=256),
     4: dict(w_dim=(1, 1, 4, 2), w_gpu_fit=1024, w_spread=0),
     5: dict(w_dim=(1, 1, 4, 2), w_gpu_fit=1024, w_spread=0),
 }

@@ -406,3 +406,16 @@ def test_place_widest_rows_parity(oracle, placer):
     p = _abi.default_params(**synth.CONFIG_PARAMS[3])
     g, o = _place_both(oracle, placer, w, p)
     _assert_same(g, o, "widest rows")
+
+
+def test_config1_runner_gpu(oracle, placer):
+    """BASELINE config #1: the reference's sample CRs + synthetic CRs and Node
+    reports through packer -> kp_place (GPU) -> status writer; every CR's
+    Placed condition equals the oracle-backed run of the same batch."""
+    from test_host import OraclePlacer, run_config1
+    _, _, got, s_gpu, _ = run_config1(placer)
+    _, _, want, s_cpu, _ = run_config1(OraclePlacer(oracle))
+    strip = lambda d: {k: [{kk: vv for kk, vv in c.items() if kk != "lastUpdateTime"}
+                           for c in v["conditions"]] for k, v in d.items()}
+    assert strip(got) == strip(want)
+    assert (s_gpu["placed"], s_gpu["rounds"]) == (s_cpu["placed"], s_cpu["rounds"])
