@@ -71,11 +71,6 @@ static int dalloc(T **p, size_t n) {
   return KP_OK;
 }
 
-#define KP_TRY(expr)          \
-  do {                        \
-    int rc_ = (expr);         \
-    if (rc_ != KP_OK) return rc_; \
-  } while (0)
 
 static int ensure_nodes(kp_ctx *c, int32_t N, int32_t D) {
   if (N <= c->cap_N && D == c->D && c->d.cap) return KP_OK;
@@ -91,6 +86,7 @@ static int ensure_nodes(kp_ctx *c, int32_t N, int32_t D) {
   KP_TRY(dalloc(&c->d.roff, (size_t)n + 1));
   KP_TRY(dalloc(&c->d.node_flag, (size_t)n));
   KP_TRY(dalloc(&c->d.node_list, (size_t)n));
+  KP_TRY(dalloc(&c->d.np32, (size_t)(4 * D + 1) * (((size_t)n + 1023) & ~(size_t)1023)));
   c->cap_N = n;
   return KP_OK;
 }
@@ -157,9 +153,11 @@ static int ensure_units(kp_ctx *c, int32_t U, int32_t J) {
 }
 
 static int ensure_q(kp_ctx *c, int32_t U, int32_t D) {
-  static thread_local int32_t dummy;
-  (void)dummy;
-  return dalloc(&c->d.q, (size_t)D * std::max(U, 1));
+  const int64_t n = (int64_t)D * std::max(U, 64);
+  if (n <= c->cap_q && c->d.q) return KP_OK;  // grows only
+  KP_TRY(dalloc(&c->d.q, (size_t)n));
+  c->cap_q = n;
+  return KP_OK;
 }
 
 static int ensure_matrix(kp_ctx *c, int32_t rows) {
@@ -281,6 +279,9 @@ int kp_create(kp_ctx **out, const kp_config *cfg) {
   c->max_pairs_matrix = cfg->max_pairs_matrix;
   if (const char *e = std::getenv("KP_SELECT_LDS_CAP")) c->select_lds_cap = std::atoi(e);
   if (const char *e = std::getenv("KP_SELECT_GENERIC")) c->select_generic = std::atoi(e) != 0;
+  if (const char *e = std::getenv("KP_SCORE_WG_TARGET")) c->score_wg_target = std::max(64, std::atoi(e));
+  if (const char *e = std::getenv("KP_SCORE_MIN_RPB")) c->score_min_rpb = std::max(1, std::atoi(e));
+  if (const char *e = std::getenv("KP_SCORE_NPL")) c->score_npl = std::atoi(e) == 4 ? 4 : 2;
   if (hipSetDevice(dev) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void **>(&c->pinned), 4096, hipHostMallocDefault) !=
@@ -318,7 +319,7 @@ void kp_destroy(kp_ctx *c) {
                   d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
                   d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.roff,
                   d.rreq, d.rsuf, d.rprio, d.pre_node, d.pre_vict, d.pre_cost,
-                  d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.stats};
+                  d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.stats, d.np32};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->world > 1) {
@@ -822,6 +823,7 @@ int kp_score(kp_ctx *c, const kp_params *p, int32_t job_lo, int32_t job_hi, int3
   KP_TRY(ensure_matrix(c, (int32_t)std::min<int64_t>(rows, rpc)));
   std::vector<int32_t> hs;
   std::vector<uint64_t> hm;
+  KP_TRY(launch_pack(c));  // 32-bit node planes of the current usage
   for (int64_t r0 = 0; r0 < rows; r0 += rpc) {
     const int32_t nr = (int32_t)std::min<int64_t>(rpc, rows - r0);
     KP_HIP(hipMemcpyAsync(c->d.act_local, unit_of.data() + r0, sizeof(int32_t) * nr,

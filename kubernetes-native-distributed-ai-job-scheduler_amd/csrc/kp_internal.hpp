@@ -53,6 +53,7 @@ struct DevState {
   uint64_t *R = nullptr;  // floor(S*2^32/cap), 0 if cap == 0
   int64_t *base = nullptr;
   int32_t *topo = nullptr;
+  uint32_t *np32 = nullptr;  // [4*D+1][round_up(N,1024)] 32-bit score tile planes (k_pack32)
   // units (rank order), job outputs
   int64_t *q = nullptr;  // [D][U]
   int32_t *leader = nullptr, *size = nullptr, *status = nullptr;
@@ -126,9 +127,13 @@ struct kp_ctx {
   // generic per-lane top-K select
   int32_t select_lds_cap = 0;
   bool select_generic = false;
+  // score launch geometry (tuning knobs): target workgroups per launch and
+  // the smallest number of job rows per workgroup
+  int32_t score_wg_target = 2048, score_min_rpb = 4, score_npl = 2;
   // sizes
   int32_t N = 0, D = 0, J = 0, U = 0, R = 0, cap_R = 0, cap_delta = 0;
   int32_t cap_N = 0, cap_U = 0, cap_J = 0, cap_rows = 0, cap_props = 0, cap_K = 0;
+  int64_t cap_q = 0;           // int64 entries of d.q
   int32_t u_lo = 0, u_hi = 0;  // this rank's shard of units (rank positions)
   bool nodes_loaded = false, jobs_loaded = false, solved = false;
   // every cap and every req < 2^32: the filter+score pass may run in 32-bit
@@ -152,6 +157,10 @@ struct kp_ctx {
 // Kernel launchers (kp_score.hip, kp_pass.hip).
 namespace kp {
 int launch_prep_nodes(kp_ctx *c, int32_t S, int most_allocated, const int32_t *w);
+// 32-bit node planes (d.np32) of the current usage; k_score32 reads them, so
+// every caller of launch_score packs first (the solve does it in the fused
+// round-start kernel of launch_active / launch_active_async)
+int launch_pack(kp_ctx *c);
 // Kernels that take a device count pointer (rows_dev / A_dev, nullable) size
 // their grid by the host bound and clamp to the device count, so a round can
 // be enqueued before the host knows its exact number of active units.
@@ -187,3 +196,9 @@ int launch_delta(kp_ctx *c, int32_t K, int32_t *bad_host);
   } while (0)
 
 void kp_set_error(const char *what, hipError_t e);
+
+#define KP_TRY(expr)              \
+  do {                            \
+    int rc_ = (expr);             \
+    if (rc_ != KP_OK) return rc_; \
+  } while (0)

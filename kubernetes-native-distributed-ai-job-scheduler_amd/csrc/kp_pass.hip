@@ -103,63 +103,63 @@ __global__ void k_csr_finish(int32_t P, int32_t N, int32_t K, int32_t D, int32_t
 // subtracts the spread penalty of its topo domain, and the group takes the
 // (max value, lowest lane). All first-level loads (slot state, unit, candidate,
 // entry index) are issued together, before the open test.
+struct PlanArgs {
+  ScoreParams sp;
+  int32_t A;
+  const int32_t *A_dev;
+  int32_t U, pass;
+  const int32_t *act, *cand, *inv;
+  uint8_t *open;
+  int32_t *status;
+  const int64_t *cap, *used;
+  const uint64_t *R;
+  const int64_t *base;
+  const int32_t *topo;
+  const int64_t *q;
+  const int32_t *size;
+  uint32_t *bid;
+  int32_t *win, *s0_out, *pass_flag;
+  int4 *gpart;
+  int32_t *nparts, *arrive, *node_flag;
+};
+
+// the slots of wave `wave_global` (whole wave; A = the clamped slot count)
 template <int D, int G>
-__global__ __launch_bounds__(256) void k_plan(ScoreParams sp, int32_t A, const int32_t *__restrict__ A_dev,
-                                              int32_t U, int32_t pass,
-                                              const int32_t *__restrict__ act,
-                                              const int32_t *__restrict__ cand,
-                                              const int32_t *__restrict__ inv,
-                                              uint8_t *__restrict__ open,
-                                              int32_t *__restrict__ status,
-                                              const int64_t *__restrict__ cap,
-                                              const int64_t *__restrict__ used,
-                                              const uint64_t *__restrict__ R,
-                                              const int64_t *__restrict__ base,
-                                              const int32_t *__restrict__ topo,
-                                              const int64_t *__restrict__ q,
-                                              const int32_t *__restrict__ size,
-                                              uint32_t *__restrict__ bid,
-                                              int32_t *__restrict__ win,
-                                              int32_t *__restrict__ s0_out,
-                                              int32_t *__restrict__ pass_flag,
-                                              int4 *__restrict__ gpart,
-                                              int32_t *__restrict__ nparts,
-                                              int32_t *__restrict__ arrive,
-                                              int32_t *__restrict__ node_flag) {
+__device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t A, int32_t pass,
+                                          int wave_global) {
   constexpr int SPW = 64 / G;  // slots per wave
   constexpr uint64_t GMASK = G == 64 ? ~0ull : ((1ull << G) - 1);
+  const ScoreParams &sp = pa.sp;
   const int lane = threadIdx.x & 63;
   const int gl = lane & (G - 1);      // lane within the group = candidate index
   const int gbase = lane & ~(G - 1);  // first lane of the group
-  const int wave_global = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int a = wave_global * SPW + lane / G;
-  const int K = sp.n_cand, N = sp.N;
-  if (A_dev) A = min(A, *A_dev);
+  const int K = sp.n_cand, N = sp.N, U = pa.U;
   const bool in = a < A;
   const int aa = in ? a : 0;  // A > 0: slot 0 exists
-  const uint8_t op = open[aa];
-  const int32_t u0 = act[aa];
-  const int32_t node = gl < K ? cand[(int64_t)aa * K + gl] : -1;
-  const int32_t e_inv = gl < K ? inv[(int64_t)aa * K + gl] : 0;  // valid iff node >= 0
+  const uint8_t op = pa.open[aa];
+  const int32_t u0 = pa.act[aa];
+  const int32_t node = gl < K ? pa.cand[(int64_t)aa * K + gl] : -1;
+  const int32_t e_inv = gl < K ? pa.inv[(int64_t)aa * K + gl] : 0;  // valid iff node >= 0
   const bool slot_ok = in && op;
   if (__ballot(slot_ok) == 0) return;
   const int32_t u = slot_ok ? u0 : 0;
-  const int32_t sz = slot_ok ? size[u] : 0;
+  const int32_t sz = slot_ok ? pa.size[u] : 0;
   int64_t qq[D];
 #pragma unroll
-  for (int d = 0; d < D; ++d) qq[d] = slot_ok ? q[(int64_t)d * U + u] : 0;
+  for (int d = 0; d < D; ++d) qq[d] = slot_ok ? pa.q[(int64_t)d * U + u] : 0;
   const bool valid = slot_ok && node >= 0;
   const int nn = valid ? node : 0;
   int64_t c_[D], u0_[D];
   uint64_t r_[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    c_[d] = cap[(int64_t)d * N + nn];
-    u0_[d] = used[(int64_t)d * N + nn];
-    r_[d] = R[(int64_t)d * N + nn];
+    c_[d] = pa.cap[(int64_t)d * N + nn];
+    u0_[d] = pa.used[(int64_t)d * N + nn];
+    r_[d] = pa.R[(int64_t)d * N + nn];
   }
-  const int64_t b = base[nn];
-  const int32_t tp = topo[nn];
+  const int64_t b = pa.base[nn];
+  const int32_t tp = pa.topo[nn];
   int32_t szmax = sz;
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) szmax = max(szmax, __shfl_xor(szmax, m, kWave));
@@ -199,28 +199,34 @@ __global__ __launch_bounds__(256) void k_plan(ScoreParams sp, int32_t A, const i
   if (!slot_ok) return;
   if (fail) {
     if (gl == 0) {
-      open[a] = 0;
-      if (pass == 0) status[u] = kNoFit;
+      pa.open[a] = 0;
+      if (pass == 0) pa.status[u] = kNoFit;
     }
     return;
   }
   if (prop) {
-    bid[e_inv] = ((uint32_t)pass << 8) | (uint32_t)planned;
-    s0_out[e_inv] = s0;
-    win[e_inv >> 6] = pass;
-    node_flag[node] = pass;
+    pa.bid[e_inv] = ((uint32_t)pass << 8) | (uint32_t)planned;
+    pa.s0_out[e_inv] = s0;
+    pa.win[e_inv >> 6] = pass;
+    pa.node_flag[node] = pass;
     if (np > 1) {
       const int idx = __popcll(pm & ((1ull << gl) - 1));
-      gpart[(int64_t)a * K + idx] = make_int4(node, planned, inc - planned, s0);
+      pa.gpart[(int64_t)a * K + idx] = make_int4(node, planned, inc - planned, s0);
     }
   }
   if (gl == 0) {
-    pass_flag[pass] = 1;
+    pa.pass_flag[pass] = 1;
     if (np > 1) {
-      nparts[a] = np;
-      arrive[a] = 0;
+      pa.nparts[a] = np;
+      pa.arrive[a] = 0;
     }
   }
+}
+
+template <int D, int G>
+__global__ __launch_bounds__(256) void k_plan(PlanArgs pa) {
+  const int32_t A = pa.A_dev ? min(pa.A, *pa.A_dev) : pa.A;
+  plan_wave<D, G>(pa, A, pa.pass, blockIdx.x * 4 + (threadIdx.x >> 6));
 }
 
 // ---- accept ----------------------------------------------------------------------
@@ -351,40 +357,32 @@ __device__ __forceinline__ void decide_window(const Win<D> &wc, int64_t (&rem)[D
   }
 }
 
+struct AccArgs {
+  ScoreParams sp;
+  int64_t P;
+  const int32_t *seg_start, *seg_end;
+  const uint32_t *bid;
+  const int32_t *win, *s0;
+  const int64_t *ent_q;
+  const int32_t *ent_unit, *ent_size, *ent_lead, *ent_slot;
+  const int64_t *cap;
+  const int32_t *node_flag, *node_list, *nl_count;
+  AcceptOut o;
+};
+
+// the bidders of `node` in pass `pass` (whole wave)
 template <int D>
-__global__ __launch_bounds__(256) void k_accept(ScoreParams sp, int32_t pass, int64_t P,
-                                                const int32_t *__restrict__ seg_start,
-                                                const int32_t *__restrict__ seg_end,
-                                                const uint32_t *__restrict__ bid,
-                                                const int32_t *__restrict__ win,
-                                                const int32_t *__restrict__ s0,
-                                                const int64_t *__restrict__ ent_q,
-                                                const int32_t *__restrict__ ent_unit,
-                                                const int32_t *__restrict__ ent_size,
-                                                const int32_t *__restrict__ ent_lead,
-                                                const int32_t *__restrict__ ent_slot,
-                                                const int64_t *__restrict__ cap,
-                                                const int32_t *__restrict__ node_flag,
-                                                const int32_t *__restrict__ node_list,
-                                                const int32_t *__restrict__ nl_count,
-                                                int32_t use_list, AcceptOut o) {
+__device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int node) {
   const int lane = threadIdx.x & 63;
-  const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int N = sp.N;
-  int node = wv;
-  if (use_list) {  // small rounds: one wave per node that has bidders this round
-    if (wv >= *nl_count) return;
-    node = node_list[wv];
-  } else if (node >= N) {
-    return;
-  }
-  const int32_t nf = node_flag[node];
-  const int32_t e0 = seg_start[node];
-  const int32_t e1 = seg_end[node];
+  const int N = ac.sp.N;
+  const AcceptOut &o = ac.o;
+  const int32_t nf = ac.node_flag[node];
+  const int32_t e0 = ac.seg_start[node];
+  const int32_t e1 = ac.seg_end[node];
   int64_t rem[D], add[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    rem[d] = cap[(int64_t)d * N + node] - o.used[(int64_t)d * N + node];
+    rem[d] = ac.cap[(int64_t)d * N + node] - o.used[(int64_t)d * N + node];
     add[d] = 0;
   }
   if (nf != pass || e0 < 0) return;  // nobody bid on this node in this pass
@@ -392,7 +390,7 @@ __global__ __launch_bounds__(256) void k_accept(ScoreParams sp, int32_t pass, in
   constexpr int BATCH = 4;  // flagged windows whose operands are loaded together
   for (int wb = w0; wb <= w1; wb += 64) {
     // a one-window segment is loaded without consulting its window flag
-    uint64_t flagged = w0 == w1 ? 1ull : __ballot(wb + lane <= w1 && win[wb + lane] == pass);
+    uint64_t flagged = w0 == w1 ? 1ull : __ballot(wb + lane <= w1 && ac.win[wb + lane] == pass);
     while (flagged) {
       int wl[BATCH];
 #pragma unroll
@@ -403,8 +401,8 @@ __global__ __launch_bounds__(256) void k_accept(ScoreParams sp, int32_t pass, in
       Win<D> wv[BATCH];
 #pragma unroll
       for (int t = 0; t < BATCH; ++t)
-        load_win<D>(wv[t], wl[t], lane, e0, e1, pass, P, bid, ent_q, ent_unit, ent_size,
-                    ent_lead, ent_slot, s0);
+        load_win<D>(wv[t], wl[t], lane, e0, e1, pass, ac.P, ac.bid, ac.ent_q, ac.ent_unit,
+                    ac.ent_size, ac.ent_lead, ac.ent_slot, ac.s0);
 #pragma unroll
       for (int t = 0; t < BATCH; ++t) {
         if (wl[t] < 0) break;
@@ -422,25 +420,95 @@ __global__ __launch_bounds__(256) void k_accept(ScoreParams sp, int32_t pass, in
   }
 }
 
+// One wave per node: the nodes with bidders this round (use_list, small
+// rounds) or every node.
+template <int D>
+__global__ __launch_bounds__(256) void k_accept(AccArgs ac, int32_t pass, int32_t use_list) {
+  const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
+  int node = wv;
+  if (use_list) {
+    if (wv >= *ac.nl_count) return;
+    node = ac.node_list[wv];
+  } else if (node >= ac.sp.N) {
+    return;
+  }
+  accept_node<D>(ac, pass, node);
+}
+
+static PlanArgs plan_args(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass,
+                          const int32_t *A_dev) {
+  PlanArgs pa;
+  pa.sp = sp;
+  pa.A = A;
+  pa.A_dev = A_dev;
+  pa.U = c->U;
+  pa.pass = pass;
+  pa.act = c->d.act;
+  pa.cand = c->d.cand;
+  pa.inv = c->d.inv;
+  pa.open = c->d.open;
+  pa.status = c->d.status;
+  pa.cap = c->d.cap;
+  pa.used = c->d.used;
+  pa.R = c->d.R;
+  pa.base = c->d.base;
+  pa.topo = c->d.topo;
+  pa.q = c->d.q;
+  pa.size = c->d.size;
+  pa.bid = c->d.bid;
+  pa.win = c->d.win;
+  pa.s0_out = c->d.s0;
+  pa.pass_flag = c->d.pass_flag;
+  pa.gpart = c->d.gpart;
+  pa.nparts = c->d.nparts;
+  pa.arrive = c->d.arrive;
+  pa.node_flag = c->d.node_flag;
+  return pa;
+}
+
+static AccArgs acc_args(kp_ctx *c, const ScoreParams &sp, int64_t P) {
+  AccArgs ac;
+  ac.sp = sp;
+  ac.P = P;
+  ac.seg_start = c->d.seg_start;
+  ac.seg_end = c->d.seg_end;
+  ac.bid = c->d.bid;
+  ac.win = c->d.win;
+  ac.s0 = c->d.s0;
+  ac.ent_q = c->d.ent_q;
+  ac.ent_unit = c->d.ent_unit;
+  ac.ent_size = c->d.ent_size;
+  ac.ent_lead = c->d.ent_lead;
+  ac.ent_slot = c->d.ent_slot;
+  ac.cap = c->d.cap;
+  ac.node_flag = c->d.node_flag;
+  ac.node_list = c->d.node_list;
+  ac.nl_count = c->d.counters + 32;
+  AcceptOut &o = ac.o;
+  o.N = c->N;
+  o.U = c->U;
+  o.K = sp.n_cand;
+  o.gpart = c->d.gpart;
+  o.nparts = c->d.nparts;
+  o.arrive = c->d.arrive;
+  o.q = c->d.q;
+  o.used = c->d.used;
+  o.open = c->d.open;
+  o.status = c->d.status;
+  o.job_node = c->d.job_node;
+  o.job_score = c->d.job_score;
+  return ac;
+}
+
 template <int D>
 struct PlanL {
   static int run(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass,
                  const int32_t *A_dev) {
-    if (sp.n_cand <= 16) {
-      constexpr int G = 16;
-      hipLaunchKernelGGL((k_plan<D, G>), dim3(blocks(A, 4 * (64 / G))), dim3(256), 0, c->stream,
-                         sp, A, A_dev, c->U, pass, c->d.act, c->d.cand, c->d.inv, c->d.open,
-                         c->d.status, c->d.cap, c->d.used, c->d.R, c->d.base, c->d.topo, c->d.q,
-                         c->d.size, c->d.bid, c->d.win, c->d.s0, c->d.pass_flag, c->d.gpart,
-                         c->d.nparts, c->d.arrive, c->d.node_flag);
-    } else {
-      constexpr int G = 32;
-      hipLaunchKernelGGL((k_plan<D, G>), dim3(blocks(A, 4 * (64 / G))), dim3(256), 0, c->stream,
-                         sp, A, A_dev, c->U, pass, c->d.act, c->d.cand, c->d.inv, c->d.open,
-                         c->d.status, c->d.cap, c->d.used, c->d.R, c->d.base, c->d.topo, c->d.q,
-                         c->d.size, c->d.bid, c->d.win, c->d.s0, c->d.pass_flag, c->d.gpart,
-                         c->d.nparts, c->d.arrive, c->d.node_flag);
-    }
+    const PlanArgs pa = plan_args(c, sp, A, pass, A_dev);
+    if (sp.n_cand <= 16)
+      hipLaunchKernelGGL((k_plan<D, 16>), dim3(blocks(A, 4 * 4)), dim3(256), 0, c->stream, pa);
+    else
+      hipLaunchKernelGGL((k_plan<D, 32>), dim3(blocks(A, 4 * 2)), dim3(256), 0, c->stream, pa);
     KP_HIP(hipGetLastError());
     return KP_OK;
   }
@@ -449,26 +517,12 @@ struct PlanL {
 template <int D>
 struct AcceptL {
   static int run(kp_ctx *c, const ScoreParams &sp, int32_t pass, int64_t P) {
-    AcceptOut o;
-    o.N = c->N;
-    o.U = c->U;
-    o.K = sp.n_cand;
-    o.gpart = c->d.gpart;
-    o.nparts = c->d.nparts;
-    o.arrive = c->d.arrive;
-    o.q = c->d.q;
-    o.used = c->d.used;
-    o.open = c->d.open;
-    o.status = c->d.status;
-    o.job_node = c->d.job_node;
-    o.job_score = c->d.job_score;
+    const AccArgs ac = acc_args(c, sp, P);
     // rounds with fewer bidder entries than nodes walk the active-node list
     const int32_t use_list = P < c->N ? 1 : 0;
     const int64_t waves = use_list ? P : c->N;
-    hipLaunchKernelGGL((k_accept<D>), dim3(blocks(waves, 4)), dim3(256), 0, c->stream, sp, pass,
-                       P, c->d.seg_start, c->d.seg_end, c->d.bid, c->d.win, c->d.s0, c->d.ent_q,
-                       c->d.ent_unit, c->d.ent_size, c->d.ent_lead, c->d.ent_slot, c->d.cap,
-                       c->d.node_flag, c->d.node_list, c->d.counters + 32, use_list, o);
+    hipLaunchKernelGGL((k_accept<D>), dim3(blocks(waves, 4)), dim3(256), 0, c->stream, ac, pass,
+                       use_list);
     KP_HIP(hipGetLastError());
     return KP_OK;
   }

@@ -125,7 +125,7 @@ __device__ __forceinline__ uint64_t spread4_16(uint64_t x) {
   return x;
 }
 
-constexpr int kScoreMaxRows = 32;  // rows per workgroup (LDS request stage)
+constexpr int kScoreMaxRows = 128;  // rows per workgroup (LDS request stage)
 
 // v_mul_u32_u24 as written: the compiler otherwise fuses the 24-bit product
 // with the mulhi sum into a (much slower) v_mad_u64_u32
@@ -135,64 +135,149 @@ __device__ __forceinline__ uint32_t mul_u24(uint32_t a, uint32_t b) {
   return r;
 }
 
-template <int D, bool MOST>
+// bits [47:32] of the 48-bit product of two 24-bit operands (full rate)
+__device__ __forceinline__ uint32_t mulhi_u24(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// Round-start pack of the node table into the 32-bit form k_score32 consumes:
+// u32 SoA planes [4*d + {0: free, 1: used, 2: R lo, 3: R hi}][P] and the
+// LeastAllocated base in plane 4*D, P = round_up(N, 1024) (whole score tiles;
+// padding nodes are zero and masked in the kernel). One 16-B load per lane
+// and plane then fetches a lane's 4 consecutive nodes: 4*D+1 fully coalesced
+// loads per wave instead of 3*D*4 strided 8-B gathers from the int64 table.
+template <int D>
+__device__ __forceinline__ void pack_node(const int64_t *__restrict__ cap,
+                                          const int64_t *__restrict__ used,
+                                          const uint64_t *__restrict__ R,
+                                          const int64_t *__restrict__ base, int32_t N, int32_t P,
+                                          uint32_t *__restrict__ np, int n) {
+  const bool v = n < N;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const int64_t cc = v ? cap[(int64_t)d * N + n] : 0, uu = v ? used[(int64_t)d * N + n] : 0;
+    const uint64_t rr = v ? R[(int64_t)d * N + n] : 0;
+    np[(int64_t)(4 * d + 0) * P + n] = (uint32_t)(cc - uu);
+    np[(int64_t)(4 * d + 1) * P + n] = (uint32_t)uu;
+    np[(int64_t)(4 * d + 2) * P + n] = (uint32_t)rr;
+    np[(int64_t)(4 * d + 3) * P + n] = (uint32_t)(rr >> 32);
+  }
+  np[(int64_t)(4 * D) * P + n] = v ? (uint32_t)base[n] : 0u;
+}
+
+// Round start, one launch: active-unit flags of [lo, hi) (input of the
+// compaction) and, when P > 0, the 32-bit node planes of the usage the round
+// scores against.
+template <int D>
+__global__ __launch_bounds__(256) void k_round_start(const int32_t *__restrict__ status,
+                                                     int32_t lo, int32_t hi,
+                                                     int32_t *__restrict__ flag,
+                                                     const int64_t *__restrict__ cap,
+                                                     const int64_t *__restrict__ used,
+                                                     const uint64_t *__restrict__ R,
+                                                     const int64_t *__restrict__ base, int32_t N,
+                                                     int32_t P, uint32_t *__restrict__ np) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < hi - lo) flag[i] = status[lo + i] == kActive ? 1 : 0;
+  if (i < P) pack_node<D>(cap, used, R, base, N, P, np, i);
+}
+
+// bit j of a 32-bit value -> bit 2j
+__device__ __forceinline__ uint64_t spread2_32(uint64_t x) {
+  x &= 0xFFFFFFFFull;
+  x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+  x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+  x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  x = (x | (x << 2)) & 0x3333333333333333ull;
+  x = (x | (x << 1)) & 0x5555555555555555ull;
+  return x;
+}
+
+template <int NPL>
+struct Vec;  // NPL consecutive u32 per lane: one 8- or 16-B access
+template <>
+struct Vec<2> {
+  using T = uint2;
+  static __device__ __forceinline__ uint32_t at(const T &v, int k) { return k ? v.y : v.x; }
+};
+template <>
+struct Vec<4> {
+  using T = uint4;
+  static __device__ __forceinline__ uint32_t at(const T &v, int k) {
+    return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
+  }
+};
+
+template <int D, bool MOST, int NPL>
 __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
-                                                 const int64_t *__restrict__ cap,
-                                                 const int64_t *__restrict__ used,
-                                                 const uint64_t *__restrict__ R,
-                                                 const int64_t *__restrict__ base,
+                                                 const uint32_t *__restrict__ np, int32_t P,
                                                  const int64_t *__restrict__ q, int32_t qstride,
                                                  const int32_t *__restrict__ rows_unit,
                                                  int32_t rows, int32_t rows_per_block,
                                                  int32_t *__restrict__ score,
                                                  uint64_t *__restrict__ mask, int32_t Ns,
                                                  const int32_t *__restrict__ rows_dev) {
-  constexpr int NPL = 4;
+  static_assert(NPL == 2 || NPL == 4, "2 or 4 nodes per lane");
+  using V = Vec<NPL>;
   if (rows_dev) rows = min(rows, *rows_dev);
   if ((int)blockIdx.y * rows_per_block >= rows) return;  // block-uniform
   __shared__ uint32_t sq[kScoreMaxRows][D + 1];  // [D] = request in the GPU dim (0 if none)
   const int N = sp.N;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int tile0 = blockIdx.x * 1024 + wave * 256;
-  const int nb = tile0 + lane * NPL;  // first of this lane's 4 nodes
+  const int tile0 = blockIdx.x * (256 * NPL) + wave * (64 * NPL);
+  const int nb = tile0 + lane * NPL;  // first of this lane's NPL nodes
   const int r0 = blockIdx.y * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
   const int g = sp.gpu_dim;
-  if ((int)threadIdx.x < (r1 - r0) * (D + 1)) {
-    const int rr = threadIdx.x / (D + 1), d = threadIdx.x % (D + 1);
+  for (int i = threadIdx.x; i < (r1 - r0) * (D + 1); i += blockDim.x) {
+    const int rr = i / (D + 1), d = i % (D + 1);
     const int dd = d < D ? d : g;
     sq[rr][d] = dd >= 0 ? (uint32_t)q[(int64_t)dd * qstride + rows_unit[r0 + rr]] : 0u;
   }
   uint32_t f_[NPL][D], u_[NPL][D], rl_[NPL][D], rh_[NPL][D], fg_[NPL];
   int32_t b_[NPL];
   bool v_[NPL];
+  {
+    const typename V::T *pv = reinterpret_cast<const typename V::T *>(np);
+    const int64_t PV = P / NPL, iv = nb / NPL;  // P % 1024 == 0: the tile is inside
+    typename V::T pl[4 * D + 1];
 #pragma unroll
-  for (int k = 0; k < NPL; ++k) {
-    const int n = nb + k;
-    v_[k] = n < N;
-    const int nn = v_[k] ? n : 0;
-    fg_[k] = 0xFFFFFFFFu;  // free GPUs: never equal to a request when there is no GPU dim
+    for (int i = 0; i < 4 * D + 1; ++i) pl[i] = pv[i * PV + iv];
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const int64_t cc = cap[(int64_t)d * N + nn], uu = used[(int64_t)d * N + nn];
-      const uint64_t rr = R[(int64_t)d * N + nn];
-      f_[k][d] = (uint32_t)(cc - uu);
-      u_[k][d] = (uint32_t)uu;
-      rl_[k][d] = (uint32_t)rr;
-      rh_[k][d] = (uint32_t)(rr >> 32);
-      if (d == g) fg_[k] = f_[k][d];
+    for (int k = 0; k < NPL; ++k) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        f_[k][d] = V::at(pl[4 * d], k);
+        u_[k][d] = V::at(pl[4 * d + 1], k);
+        rl_[k][d] = V::at(pl[4 * d + 2], k);
+        rh_[k][d] = V::at(pl[4 * d + 3], k);
+      }
+      v_[k] = nb + k < N;
+      b_[k] = (int32_t)V::at(pl[4 * D], k);
+      fg_[k] = 0xFFFFFFFFu;  // free GPUs: never equal to a request when there is no GPU dim
+#pragma unroll
+      for (int d = 0; d < D; ++d)
+        if (d == g) fg_[k] = f_[k][d];
     }
-    b_[k] = (int32_t)base[nn];
   }
-  // wave-uniform: does any node of this wave need the Rh term in dim d?
-  // (Rh > 0 only where cap <= S; large-capacity dims skip the multiply)
-  bool need_rh[D];
+  // Per dim, wave-uniform: does any node of this wave need the Rh term
+  // (Rh > 0 only where cap <= S; large-capacity dims skip the multiply)? Is
+  // every node's cap and R below 2^24 (then u+q <= cap < 2^24 on every
+  // feasible pair and ((u+q)*R) >> 32 is one full-rate v_mul_hi_u32_u24
+  // instead of a quarter-rate v_mul_hi_u32)?
+  bool need_rh[D], fast24[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    uint32_t any = 0;
+    uint32_t any = 0, wide = 0;
 #pragma unroll
-    for (int k = 0; k < NPL; ++k) any |= rh_[k][d];
+    for (int k = 0; k < NPL; ++k) {
+      any |= rh_[k][d];
+      wide |= rh_[k][d] | (rl_[k][d] >> 24) | ((f_[k][d] + u_[k][d]) >> 24);
+    }
     need_rh[d] = __ballot(any != 0) != 0;
+    fast24[d] = __ballot(wide != 0) == 0;
   }
   __syncthreads();
   if (tile0 >= Ns) return;  // wave-uniform, after the only barrier
@@ -211,7 +296,7 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
       fits[k] = v_[k];
       acc[k] = 0;
     }
-    // dim-outer: one wave-uniform branch per dim for the Rh term
+    // dim-outer: wave-uniform branches per dim for the multiply form
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       uint32_t uu[NPL], util[NPL];
@@ -219,14 +304,21 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
       for (int k = 0; k < NPL; ++k) {
         fits[k] &= qq[d] <= f_[k][d];
         uu[k] = u_[k][d] + qq[d];
-        util[k] = __umulhi(uu[k], rl_[k][d]);
       }
-      // 24-bit multiplies (full rate) are exact wherever the pair fits:
-      // rh > 0 only if cap <= S <= 1024, and then uu <= cap; w <= 65535 and
-      // util <= S. Only mulhi stays a 32-bit (quarter-rate) multiply.
-      if (need_rh[d]) {
+      if (fast24[d]) {
+        // infeasible pairs may have uu >= 2^24 (garbage util): masked below
 #pragma unroll
-        for (int k = 0; k < NPL; ++k) util[k] += mul_u24(uu[k], rh_[k][d]);
+        for (int k = 0; k < NPL; ++k) util[k] = mulhi_u24(uu[k], rl_[k][d]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < NPL; ++k) util[k] = __umulhi(uu[k], rl_[k][d]);
+        // 24-bit multiplies (full rate) are exact wherever the pair fits:
+        // rh > 0 only if cap <= S <= 1024, and then uu <= cap; w <= 65535
+        // and util <= S
+        if (need_rh[d]) {
+#pragma unroll
+          for (int k = 0; k < NPL; ++k) util[k] += mul_u24(uu[k], rh_[k][d]);
+        }
       }
 #pragma unroll
       for (int k = 0; k < NPL; ++k) acc[k] += (int32_t)__umul24((uint32_t)sp.w[d], util[k]);
@@ -239,17 +331,28 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
       const int32_t s = (MOST ? acc[k] : b_[k] - acc[k]) + bonus;
       sv[k] = fits[k] ? s : KP_SCORE_INFEASIBLE;
     }
-    if (score && store_ok)
-      *reinterpret_cast<int4 *>(score + (int64_t)r * Ns + nb) =
-          make_int4(sv[0], sv[1], sv[2], sv[3]);
+    if (score && store_ok) {
+      if constexpr (NPL == 4)
+        *reinterpret_cast<int4 *>(score + (int64_t)r * Ns + nb) =
+            make_int4(sv[0], sv[1], sv[2], sv[3]);
+      else
+        *reinterpret_cast<int2 *>(score + (int64_t)r * Ns + nb) = make_int2(sv[0], sv[1]);
+    }
     if (mask) {  // wave-uniform: the solve passes no mask (the -1 sentinel is the filter)
       uint64_t bal[NPL];
 #pragma unroll
       for (int k = 0; k < NPL; ++k) bal[k] = __ballot(fits[k]);
-      if (lane < 4 && tile0 + 64 * lane < Ns) {
-        const int sh = 16 * lane;
-        const uint64_t wd = spread4_16(bal[0] >> sh) | (spread4_16(bal[1] >> sh) << 1) |
-                            (spread4_16(bal[2] >> sh) << 2) | (spread4_16(bal[3] >> sh) << 3);
+      // word i of the wave's tile: bit NPL*j + k = ballot_k bit (64/NPL)*i + j
+      if (lane < NPL && tile0 + 64 * lane < Ns) {
+        uint64_t wd = 0;
+        if constexpr (NPL == 4) {
+          const int sh = 16 * lane;
+          wd = spread4_16(bal[0] >> sh) | (spread4_16(bal[1] >> sh) << 1) |
+               (spread4_16(bal[2] >> sh) << 2) | (spread4_16(bal[3] >> sh) << 3);
+        } else {
+          const int sh = 32 * lane;
+          wd = spread2_32(bal[0] >> sh) | (spread2_32(bal[1] >> sh) << 1);
+        }
         mask[(int64_t)r * words + (tile0 >> 6) + lane] = wd;
       }
     }
@@ -531,12 +634,6 @@ __global__ void k_reset_units(int32_t *__restrict__ status, int32_t U,
   }
 }
 
-__global__ void k_flag_active(const int32_t *__restrict__ status, int32_t lo, int32_t hi,
-                              int32_t *__restrict__ flag) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < hi - lo) flag[i] = status[lo + i] == kActive ? 1 : 0;
-}
-
 __global__ void k_finalize(const int32_t *__restrict__ status, const int32_t *__restrict__ leader,
                            const int32_t *__restrict__ size, int32_t U,
                            int32_t *__restrict__ job_node, int32_t *__restrict__ job_score,
@@ -617,20 +714,26 @@ struct ScoreL {
                  const int32_t *rows_dev) {
     const int Ns = (c->N + 63) & ~63;
     if (c->fits32) {
+      const int P = (c->N + 1023) & ~1023;  // planes from the round start (launch_pack)
       // rows per workgroup: enough workgroups to cover the 256 CUs several
       // times over, at most kScoreMaxRows (the LDS request stage)
-      const int tiles = blocks(Ns, 1024);
-      const int64_t want = ((int64_t)rows * tiles + 2047) / 2048;
-      const int rpb = (int)std::min<int64_t>(kScoreMaxRows, std::max<int64_t>(4, want));
+      // nodes per lane: 2 (8-B stores, half the tile registers: twice the
+      // resident waves) unless KP_SCORE_NPL=4
+      const int npl = c->score_npl;
+      const int tiles = blocks(Ns, 256 * npl);
+      const int64_t want = ((int64_t)rows * tiles + c->score_wg_target - 1) / c->score_wg_target;
+      const int rpb =
+          (int)std::min<int64_t>(kScoreMaxRows, std::max<int64_t>(c->score_min_rpb, want));
       dim3 grid(tiles, blocks(rows, rpb));
-      if (sp.most_allocated)
-        hipLaunchKernelGGL((k_score32<D, true>), grid, dim3(256), 0, c->stream, sp, c->d.cap,
-                           c->d.used, c->d.R, c->d.base, q, qstride, rows_unit, rows, rpb, score,
-                           mask, Ns, rows_dev);
-      else
-        hipLaunchKernelGGL((k_score32<D, false>), grid, dim3(256), 0, c->stream, sp, c->d.cap,
-                           c->d.used, c->d.R, c->d.base, q, qstride, rows_unit, rows, rpb, score,
-                           mask, Ns, rows_dev);
+#define KP_SC32(M, NP)                                                                      \
+  hipLaunchKernelGGL((k_score32<D, M, NP>), grid, dim3(256), 0, c->stream, sp, c->d.np32, P, q, \
+                     qstride, rows_unit, rows, rpb, score, mask, Ns, rows_dev)
+      if (sp.most_allocated) {
+        if (npl == 4) KP_SC32(true, 4); else KP_SC32(true, 2);
+      } else {
+        if (npl == 4) KP_SC32(false, 4); else KP_SC32(false, 2);
+      }
+#undef KP_SC32
     } else {
       constexpr int NPL = D <= 4 ? 2 : 1;
       const int rpb = 32;
@@ -719,15 +822,34 @@ int launch_open_init(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev) {
   return KP_OK;
 }
 
+template <int D>
+struct RoundStartL {
+  static int run(kp_ctx *c, int32_t lo, int32_t hi, int32_t *flag) {
+    const int32_t P = c->fits32 && c->N > 0 ? (c->N + 1023) & ~1023 : 0;
+    const int64_t n = std::max<int64_t>(hi - lo, P);
+    if (n <= 0) return KP_OK;
+    hipLaunchKernelGGL((k_round_start<D>), dim3(blocks(n, 256)), dim3(256), 0, c->stream,
+                       c->d.status, lo, hi, flag, c->d.cap, c->d.used, c->d.R, c->d.base, c->N, P,
+                       c->d.np32);
+    KP_HIP(hipGetLastError());
+    return KP_OK;
+  }
+};
+
+// round start: active flags of [lo, hi) + (32-bit path) the node planes
+static int launch_round_start(kp_ctx *c, int32_t lo, int32_t hi, int32_t *flag) {
+  return dispatch_D<RoundStartL>(c->D, c, lo, hi, flag);
+}
+
+int launch_pack(kp_ctx *c) { return launch_round_start(c, 0, 0, nullptr); }
+
 // active units of [lo, hi) in rank order -> act_local; count to host
 int launch_active(kp_ctx *c, int32_t lo, int32_t hi, int32_t *A_host) {
   *A_host = 0;
   const int32_t n = hi - lo;
   if (n <= 0) return KP_OK;
   int32_t *flag = c->d.flag;
-  hipLaunchKernelGGL(k_flag_active, dim3(blocks(n, 256)), dim3(256), 0, c->stream, c->d.status,
-                     lo, hi, flag);
-  KP_HIP(hipGetLastError());
+  KP_TRY(launch_round_start(c, lo, hi, flag));
   size_t tb = c->d.temp_bytes;
   KP_HIP(rocprim::select(c->d.temp, tb, rocprim::counting_iterator<int32_t>(lo), flag,
                          c->d.act_local, c->d.counters, (size_t)n, c->stream));
@@ -766,9 +888,7 @@ int launch_delta(kp_ctx *c, int32_t K, int32_t *bad_host) {
 int launch_active_async(kp_ctx *c, int32_t lo, int32_t hi, int32_t *count_host) {
   const int32_t n = hi - lo;
   if (n <= 0) return KP_EINVAL;
-  hipLaunchKernelGGL(k_flag_active, dim3(blocks(n, 256)), dim3(256), 0, c->stream, c->d.status,
-                     lo, hi, c->d.flag);
-  KP_HIP(hipGetLastError());
+  KP_TRY(launch_round_start(c, lo, hi, c->d.flag));
   size_t tb = c->d.temp_bytes;
   KP_HIP(rocprim::select(c->d.temp, tb, rocprim::counting_iterator<int32_t>(lo), c->d.flag,
                          c->d.act_local, c->d.counters, (size_t)n, c->stream));
