@@ -141,6 +141,41 @@ __device__ __forceinline__ int64_t score_at(const ScoreParams &sp, const int64_t
   return fits ? s : -1;
 }
 
+// 32-bit group max (same DPP pattern as group_max_i64)
+template <int G>
+__device__ __forceinline__ int32_t group_max_i32(int32_t v) {
+  static_assert(G == 16 || G == 32 || G == 64, "group size");
+  const int l = lane_id(), rl = l & 15;
+  int32_t t;
+  t = __builtin_amdgcn_mov_dpp(v, 0x111, 0xf, 0xf, false);
+  if (rl >= 1) v = max(v, t);
+  t = __builtin_amdgcn_mov_dpp(v, 0x112, 0xf, 0xf, false);
+  if (rl >= 2) v = max(v, t);
+  t = __builtin_amdgcn_mov_dpp(v, 0x114, 0xf, 0xf, false);
+  if (rl >= 4) v = max(v, t);
+  t = __builtin_amdgcn_mov_dpp(v, 0x118, 0xf, 0xf, false);
+  if (rl >= 8) v = max(v, t);
+  if (G >= 32) {
+    t = __builtin_amdgcn_mov_dpp(v, 0x142, 0xf, 0xf, false);  // row_bcast:15
+    if ((l & 31) >= 16) v = max(v, t);
+  }
+  if (G >= 64) {
+    t = __builtin_amdgcn_mov_dpp(v, 0x143, 0xf, 0xf, false);  // row_bcast:31
+    if (l >= 32) v = max(v, t);
+  }
+  if (G == 16) {
+    const int32_t m0 = __builtin_amdgcn_readlane(v, 15), m1 = __builtin_amdgcn_readlane(v, 31);
+    const int32_t m2 = __builtin_amdgcn_readlane(v, 47), m3 = __builtin_amdgcn_readlane(v, 63);
+    const int g = l >> 4;
+    return g == 0 ? m0 : g == 1 ? m1 : g == 2 ? m2 : m3;
+  }
+  if (G == 32) {
+    const int32_t m0 = __builtin_amdgcn_readlane(v, 31), m1 = __builtin_amdgcn_readlane(v, 63);
+    return l < 32 ? m0 : m1;
+  }
+  return __builtin_amdgcn_readlane(v, 63);
+}
+
 inline int blocks(int64_t n, int b) { return (int)((n + b - 1) / b); }
 
 template <template <int> class F, typename... Args>

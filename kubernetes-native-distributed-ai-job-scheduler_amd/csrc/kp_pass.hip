@@ -123,10 +123,11 @@ struct PlanArgs {
   int32_t *nparts, *arrive, *node_flag;
 };
 
-// the slots of wave `wave_global` (whole wave; A = the clamped slot count)
-template <int D, int G>
-__device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t A, int32_t pass,
-                                          int wave_global) {
+// the slots of wave `wave_global` (whole wave). The slot loads do not wait
+// for the device slot count: they are issued together with it (slots past the
+// count but below the host bound are readable and ignored).
+template <int D, int G, bool W32>
+__device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int wave_global) {
   constexpr int SPW = 64 / G;  // slots per wave
   constexpr uint64_t GMASK = G == 64 ? ~0ull : ((1ull << G) - 1);
   const ScoreParams &sp = pa.sp;
@@ -135,12 +136,13 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t A, int32_t
   const int gbase = lane & ~(G - 1);  // first lane of the group
   const int a = wave_global * SPW + lane / G;
   const int K = sp.n_cand, N = sp.N, U = pa.U;
-  const bool in = a < A;
-  const int aa = in ? a : 0;  // A > 0: slot 0 exists
+  const int aa = min(a, pa.A - 1);  // host bound A > 0
   const uint8_t op = pa.open[aa];
   const int32_t u0 = pa.act[aa];
   const int32_t node = gl < K ? pa.cand[(int64_t)aa * K + gl] : -1;
   const int32_t e_inv = gl < K ? pa.inv[(int64_t)aa * K + gl] : 0;  // valid iff node >= 0
+  const int32_t A = pa.A_dev ? min(pa.A, *pa.A_dev) : pa.A;
+  const bool in = a < A;
   const bool slot_ok = in && op;
   if (__ballot(slot_ok) == 0) return;
   const int32_t u = slot_ok ? u0 : 0;
@@ -150,39 +152,92 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t A, int32_t
   for (int d = 0; d < D; ++d) qq[d] = slot_ok ? pa.q[(int64_t)d * U + u] : 0;
   const bool valid = slot_ok && node >= 0;
   const int nn = valid ? node : 0;
-  int64_t c_[D], u0_[D];
-  uint64_t r_[D];
-#pragma unroll
-  for (int d = 0; d < D; ++d) {
-    c_[d] = pa.cap[(int64_t)d * N + nn];
-    u0_[d] = pa.used[(int64_t)d * N + nn];
-    r_[d] = pa.R[(int64_t)d * N + nn];
-  }
-  const int64_t b = pa.base[nn];
+  int32_t planned = 0, dom = 0, s0 = -1;
+  bool fail = !slot_ok;
   const int32_t tp = pa.topo[nn];
   int32_t szmax = sz;
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) szmax = max(szmax, __shfl_xor(szmax, m, kWave));
-  int32_t planned = 0, dom = 0, s0 = -1;
-  bool fail = !slot_ok;
-  for (int m = 0; m < szmax; ++m) {
-    const bool live = !fail && m < sz;  // group-uniform
-    int64_t uu[D];
+  if constexpr (W32) {
+    // every cap and request < 2^32 (fits32): the remaining free capacity and
+    // the usage after the planned members are tracked incrementally, so no
+    // product of a member count overflows; util = mulhi(x, Rl) + x*Rh is
+    // exact (k_score32) and every score fits an int32
+    uint32_t q32[D], rem[D], uu[D], rl[D], rh[D];
 #pragma unroll
-    for (int d = 0; d < D; ++d) uu[d] = u0_[d] + (int64_t)planned * qq[d];
-    const int64_t s = (live && valid) ? score_at<D>(sp, qq, c_, uu, r_, b) : -1;
-    if (m == 0) s0 = (int32_t)s;
-    const bool feas = s >= 0;
-    const int64_t val = feas ? s - (int64_t)sp.w_spread * dom : INT64_MIN;
-    const uint64_t gm = (__ballot(feas) >> gbase) & GMASK;
-    if (live && gm == 0) fail = true;
-    const int64_t best = group_max_i64<G>(val);
-    const uint64_t wm = (__ballot(feas && val == best) >> gbase) & GMASK;
-    const int w = wm ? (__ffsll((unsigned long long)wm) - 1) : 0;
-    const int32_t wtp = __shfl(tp, gbase + w, kWave);
-    if (live && !fail) {
-      planned += gl == w ? 1 : 0;
-      dom += (valid && tp == wtp) ? 1 : 0;
+    for (int d = 0; d < D; ++d) {
+      q32[d] = (uint32_t)qq[d];
+      const uint64_t rr = pa.R[(int64_t)d * N + nn];
+      uu[d] = (uint32_t)pa.used[(int64_t)d * N + nn];
+      rem[d] = (uint32_t)pa.cap[(int64_t)d * N + nn] - uu[d];
+      rl[d] = (uint32_t)rr;
+      rh[d] = (uint32_t)(rr >> 32);
+    }
+    const int32_t b = (int32_t)pa.base[nn];
+    const int g = sp.gpu_dim;
+    for (int m = 0; m < szmax; ++m) {
+      const bool live = !fail && m < sz;  // group-uniform
+      bool fits = live && valid;
+      int32_t acc = 0, bonus = 0;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        fits &= q32[d] <= rem[d];
+        const uint32_t x = uu[d] + q32[d];
+        const uint32_t util = __umulhi(x, rl[d]) + x * rh[d];
+        acc += sp.w[d] * (int32_t)util;
+        if (d == g && q32[d] > 0 && rem[d] == q32[d]) bonus = sp.w_gpu_fit;
+      }
+      const int32_t s = fits ? (sp.most_allocated ? acc : b - acc) + bonus : -1;
+      if (m == 0) s0 = s;
+      const bool feas = s >= 0;
+      const int32_t val = feas ? s - sp.w_spread * dom : INT32_MIN;
+      const uint64_t gm = (__ballot(feas) >> gbase) & GMASK;
+      if (live && gm == 0) fail = true;
+      const int32_t best = group_max_i32<G>(val);
+      const uint64_t wm = (__ballot(feas && val == best) >> gbase) & GMASK;
+      const int w = wm ? (__ffsll((unsigned long long)wm) - 1) : 0;
+      const int32_t wtp = __shfl(tp, gbase + w, kWave);
+      if (live && !fail) {
+        if (gl == w) {
+          ++planned;
+#pragma unroll
+          for (int d = 0; d < D; ++d) {
+            rem[d] -= q32[d];
+            uu[d] += q32[d];
+          }
+        }
+        dom += (valid && tp == wtp) ? 1 : 0;
+      }
+    }
+  } else {
+    int64_t c_[D], u0_[D];
+    uint64_t r_[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      c_[d] = pa.cap[(int64_t)d * N + nn];
+      u0_[d] = pa.used[(int64_t)d * N + nn];
+      r_[d] = pa.R[(int64_t)d * N + nn];
+    }
+    const int64_t b = pa.base[nn];
+    for (int m = 0; m < szmax; ++m) {
+      const bool live = !fail && m < sz;  // group-uniform
+      int64_t uu[D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) uu[d] = u0_[d] + (int64_t)planned * qq[d];
+      const int64_t s = (live && valid) ? score_at<D>(sp, qq, c_, uu, r_, b) : -1;
+      if (m == 0) s0 = (int32_t)s;
+      const bool feas = s >= 0;
+      const int64_t val = feas ? s - (int64_t)sp.w_spread * dom : INT64_MIN;
+      const uint64_t gm = (__ballot(feas) >> gbase) & GMASK;
+      if (live && gm == 0) fail = true;
+      const int64_t best = group_max_i64<G>(val);
+      const uint64_t wm = (__ballot(feas && val == best) >> gbase) & GMASK;
+      const int w = wm ? (__ffsll((unsigned long long)wm) - 1) : 0;
+      const int32_t wtp = __shfl(tp, gbase + w, kWave);
+      if (live && !fail) {
+        planned += gl == w ? 1 : 0;
+        dom += (valid && tp == wtp) ? 1 : 0;
+      }
     }
   }
   // group-uniform from here on (slot_ok and fail are per group)
@@ -223,10 +278,9 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t A, int32_t
   }
 }
 
-template <int D, int G>
+template <int D, int G, bool W32>
 __global__ __launch_bounds__(256) void k_plan(PlanArgs pa) {
-  const int32_t A = pa.A_dev ? min(pa.A, *pa.A_dev) : pa.A;
-  plan_wave<D, G>(pa, A, pa.pass, blockIdx.x * 4 + (threadIdx.x >> 6));
+  plan_wave<D, G, W32>(pa, pa.pass, blockIdx.x * 4 + (threadIdx.x >> 6));
 }
 
 // ---- accept ----------------------------------------------------------------------
@@ -426,9 +480,10 @@ template <int D>
 __global__ __launch_bounds__(256) void k_accept(AccArgs ac, int32_t pass, int32_t use_list) {
   const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
   int node = wv;
-  if (use_list) {
+  if (use_list) {  // list entry and count loaded together (wv < P < N: in bounds)
+    const int32_t nd = ac.node_list[wv];
     if (wv >= *ac.nl_count) return;
-    node = ac.node_list[wv];
+    node = nd;
   } else if (node >= ac.sp.N) {
     return;
   }
@@ -505,10 +560,18 @@ struct PlanL {
   static int run(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass,
                  const int32_t *A_dev) {
     const PlanArgs pa = plan_args(c, sp, A, pass, A_dev);
-    if (sp.n_cand <= 16)
-      hipLaunchKernelGGL((k_plan<D, 16>), dim3(blocks(A, 4 * 4)), dim3(256), 0, c->stream, pa);
-    else
-      hipLaunchKernelGGL((k_plan<D, 32>), dim3(blocks(A, 4 * 2)), dim3(256), 0, c->stream, pa);
+    // 32-bit member loop whenever every cap and request < 2^32 (fits32)
+    if (sp.n_cand <= 16) {
+      if (c->fits32)
+        hipLaunchKernelGGL((k_plan<D, 16, true>), dim3(blocks(A, 4 * 4)), dim3(256), 0, c->stream, pa);
+      else
+        hipLaunchKernelGGL((k_plan<D, 16, false>), dim3(blocks(A, 4 * 4)), dim3(256), 0, c->stream, pa);
+    } else {
+      if (c->fits32)
+        hipLaunchKernelGGL((k_plan<D, 32, true>), dim3(blocks(A, 4 * 2)), dim3(256), 0, c->stream, pa);
+      else
+        hipLaunchKernelGGL((k_plan<D, 32, false>), dim3(blocks(A, 4 * 2)), dim3(256), 0, c->stream, pa);
+    }
     KP_HIP(hipGetLastError());
     return KP_OK;
   }

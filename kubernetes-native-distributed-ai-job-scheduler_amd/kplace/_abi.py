@@ -136,7 +136,8 @@ def params_dict(p: Params) -> dict:
 
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(PKG_DIR), "libkplace.so")
+# KPLACE_LIB: an alternative build of the same library (A/B timing runs only)
+LIB_PATH = os.environ.get("KPLACE_LIB") or os.path.join(os.path.dirname(PKG_DIR), "libkplace.so")
 
 
 def load_library(path: str | None = None) -> C.CDLL:
