@@ -211,7 +211,10 @@ typedef struct kp_preemption {
  */
 int kp_preempt(kp_ctx *ctx, kp_preemption *out);
 
-/* Timing of the last kp_solve, measured with HIP events on the solve stream. */
+/* Timing of the last kp_solve, measured with HIP events on the solve stream
+ * (kp_set_profiling(ctx, 1)): the filter+score launches are bracketed; the
+ * select is not (select_ms = 0, select_bytes still counted) and accept_ms is
+ * the rest of the solve. */
 typedef struct kp_timing {
   double solve_ms;          /* whole device solve (first launch .. last)     */
   double score_ms;          /* sum of filter+score kernel time               */
