@@ -129,7 +129,8 @@ typedef struct kp_config {
   int32_t world_size;    /* 1 = single GPU; >1 = one process per GPU          */
   int32_t rank;          /* this process' rank in [0, world_size)             */
   const void *nccl_id;   /* 128-byte ncclUniqueId from kp_dist_unique_id on
-                            rank 0, broadcast by the caller; NULL if world 1  */
+                            rank 0, broadcast by the caller; NULL if world 1,
+                            or for a host-staged exchange (kp_set_allgather) */
   int64_t max_pairs_matrix; /* cap on score-matrix entries per chunk
                                (0 = library default)                         */
 } kp_config;
@@ -140,6 +141,14 @@ const char *kp_strerror(int code);
 int kp_abi_version(void);
 /* Writes the 128-byte RCCL unique id for a multi-process context. */
 int kp_dist_unique_id(void *out128);
+/* Host-staged candidate exchange for a multi-process context created without
+ * an RCCL id: `fn` all-gathers `bytes` from every rank into `recv` (rank-major,
+ * world_size * bytes) and returns 0 on success. It is called on the thread that
+ * calls kp_solve; the library stages device buffers through host memory around
+ * it. Meant for transports other than RCCL and for testing the sharded solve
+ * with several processes on one GPU (RCCL needs one GPU per rank). */
+typedef int (*kp_allgather_fn)(void *user, const void *send, size_t bytes, void *recv);
+int kp_set_allgather(kp_ctx *ctx, kp_allgather_fn fn, void *user);
 
 /*
  * One-shot placement: validate + upload the snapshot, solve, download.

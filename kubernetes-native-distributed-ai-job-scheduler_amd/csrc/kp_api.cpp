@@ -262,7 +262,6 @@ int kp_create(kp_ctx **out, const kp_config *cfg) {
   def.world_size = 1;
   if (!cfg) cfg = &def;
   if (cfg->world_size < 1 || cfg->rank < 0 || cfg->rank >= cfg->world_size) return KP_EINVAL;
-  if (cfg->world_size > 1 && !cfg->nccl_id) return KP_EINVAL;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return KP_ENODEV;
   int dev = cfg->device;
@@ -290,7 +289,7 @@ int kp_create(kp_ctx **out, const kp_config *cfg) {
     kp_destroy(c);
     return KP_EHIP;
   }
-  if (c->world > 1) {
+  if (c->world > 1 && cfg->nccl_id) {  // else: host-staged exchange (kp_set_allgather)
     ncclUniqueId id;
     std::memcpy(&id, cfg->nccl_id, sizeof id);
     ncclComm_t comm;
@@ -329,6 +328,15 @@ void kp_destroy(kp_ctx *c) {
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
+}
+
+int kp_set_allgather(kp_ctx *c, kp_allgather_fn fn, void *user) {
+  if (!c || !fn) return KP_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->world < 2 || c->nccl_comm) return KP_ESTATE;  // RCCL contexts exchange on the device
+  c->allgather = fn;
+  c->allgather_user = user;
+  return KP_OK;
 }
 
 int kp_set_profiling(kp_ctx *c, int enable) {
@@ -491,7 +499,44 @@ int kp_load_jobs(kp_ctx *c, int32_t J, const int64_t *req, const int32_t *prio,
 }
 
 // ---------------------------------------------------------------------------
+// all-gather through host memory with the caller's transport (kp_set_allgather)
+static int exchange_host(kp_ctx *c, int32_t A_local, int32_t K, int32_t *A_global) {
+  const int W = c->world;
+  std::vector<int32_t> counts(W);
+  if (c->allgather(c->allgather_user, &A_local, sizeof(int32_t), counts.data()) != 0)
+    return KP_ERCCL;
+  int32_t Umax = 0, tot = 0;
+  for (int r = 0; r < W; ++r) {
+    Umax = std::max(Umax, counts[r]);
+    tot += counts[r];
+  }
+  *A_global = tot;
+  if (tot == 0) return KP_OK;
+  const size_t per = (size_t)Umax * (K + 1);
+  try {
+    c->h_xg_send.resize(per);
+    c->h_xg_recv.resize(per * W);
+  } catch (const std::bad_alloc &) {
+    return KP_ENOMEM;
+  }
+  KP_TRY(launch_pack_exchange(c, A_local, K));
+  KP_HIP(hipMemcpyAsync(c->h_xg_send.data(), c->d.xg_send, sizeof(int32_t) * per,
+                        hipMemcpyDeviceToHost, c->stream));
+  KP_HIP(hipStreamSynchronize(c->stream));
+  if (c->allgather(c->allgather_user, c->h_xg_send.data(), sizeof(int32_t) * per,
+                   c->h_xg_recv.data()) != 0)
+    return KP_ERCCL;
+  KP_HIP(hipMemcpyAsync(c->d.xg_counts, counts.data(), sizeof(int32_t) * W,
+                        hipMemcpyHostToDevice, c->stream));
+  KP_HIP(hipMemcpyAsync(c->d.xg_recv, c->h_xg_recv.data(), sizeof(int32_t) * per * W,
+                        hipMemcpyHostToDevice, c->stream));
+  KP_TRY(launch_unpack_exchange(c, W, Umax, K));
+  KP_HIP(hipStreamSynchronize(c->stream));  // the host buffers are reused next round
+  return KP_OK;
+}
+
 static int exchange_candidates(kp_ctx *c, int32_t A_local, int32_t K, int32_t *A_global) {
+  if (!c->nccl_comm) return exchange_host(c, A_local, K, A_global);
   ncclComm_t comm = static_cast<ncclComm_t>(c->nccl_comm);
   c->pinned[0] = A_local;
   KP_HIP(hipMemcpyAsync(c->d.counters, c->pinned, sizeof(int32_t), hipMemcpyHostToDevice,
@@ -703,6 +748,7 @@ int kp_solve(kp_ctx *c, const kp_params *p, kp_result *stats) {
   if (!c) return KP_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   if (!c->nodes_loaded || !c->jobs_loaded) return KP_ESTATE;
+  if (c->world > 1 && !c->nccl_comm && !c->allgather) return KP_ESTATE;  // no exchange
   try {
     return solve_impl(c, p, stats);
   } catch (const std::bad_alloc &) {

@@ -118,6 +118,10 @@ struct kp_ctx {
   int device = 0;
   int world = 1, rank = 0;
   void *nccl_comm = nullptr;  // ncclComm_t
+  // host-staged exchange (kp_set_allgather) when world > 1 without RCCL
+  kp_allgather_fn allgather = nullptr;
+  void *allgather_user = nullptr;
+  std::vector<int32_t> h_xg_send, h_xg_recv;
   int64_t max_pairs_matrix = 0;
   hipStream_t stream = nullptr;
   bool profiling = false;

@@ -140,6 +140,10 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KPLACE_LIB") or os.path.join(os.path.dirname(PKG_DIR), "libkplace.so")
 
 
+# kp_allgather_fn: (user, send, bytes, recv) -> 0 on success
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
+
+
 def load_library(path: str | None = None) -> C.CDLL:
     """Load libkplace.so and declare every exported signature.
 
@@ -165,6 +169,7 @@ def load_library(path: str | None = None) -> C.CDLL:
         "kp_score": (C.c_int, [vp, C.POINTER(Params), C.c_int32, C.c_int32, _i32p, _u64p]),
         "kp_last_timing": (C.c_int, [vp, C.POINTER(Timing)]),
         "kp_set_profiling": (C.c_int, [vp, C.c_int]),
+        "kp_set_allgather": (C.c_int, [vp, ALLGATHER_FN, vp]),
         "kp_parse_gpu_memory": (C.c_int, [C.c_char_p, _i64p]),
         "kp_load_running": (C.c_int, [vp, C.c_int32, _i32p, _i64p, _i32p]),
         "kp_preempt": (C.c_int, [vp, C.POINTER(Preemption)]),
@@ -182,5 +187,5 @@ EXPORTED = (
     "kp_abi_version", "kp_dist_unique_id", "kp_place", "kp_load_nodes",
     "kp_load_jobs", "kp_solve", "kp_fetch", "kp_apply_delta", "kp_reset_nodes", "kp_score",
     "kp_last_timing", "kp_set_profiling", "kp_parse_gpu_memory", "kp_load_running",
-    "kp_preempt",
+    "kp_preempt", "kp_set_allgather",
 )

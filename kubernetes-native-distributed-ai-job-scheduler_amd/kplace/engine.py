@@ -60,7 +60,11 @@ class Placer:
     node table."""
 
     def __init__(self, device: int = 0, world_size: int = 1, rank: int = 0,
-                 nccl_id: bytes | None = None, max_pairs_matrix: int = 0):
+                 nccl_id: bytes | None = None, max_pairs_matrix: int = 0,
+                 allgather=None):
+        """`allgather` (multi-process without RCCL): a callable taking this
+        rank's bytes and returning every rank's bytes concatenated in rank
+        order (kp_set_allgather)."""
         cfg = _abi.Config()
         cfg.device = device
         cfg.world_size = world_size
@@ -74,6 +78,19 @@ class Placer:
         _check(lib().kp_create(C.byref(h), C.byref(cfg)), "kp_create")
         self._h = h
         self.J = self.N = self.D = 0
+        self._cb = None
+        if allgather is not None:
+            def _cb(user, send, nbytes, recv):
+                try:
+                    out = allgather(C.string_at(send, nbytes))
+                    if len(out) != nbytes * world_size:
+                        return 1
+                    C.memmove(recv, out, len(out))
+                    return 0
+                except Exception:  # never unwind through the C frames
+                    return 1
+            self._cb = _abi.ALLGATHER_FN(_cb)
+            _check(lib().kp_set_allgather(self._h, self._cb, None), "kp_set_allgather")
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -1,0 +1,78 @@
+"""Sharded multi-process solve of libkplace on the GPU, two
+ranks on one GPU: each rank scores only its shard of units, candidates are
+exchanged through kp_set_allgather (host-staged, gloo all_gather: RCCL needs
+one GPU per rank), every rank runs the replicated acceptance passes. Both
+ranks must return the oracle's placement bit for bit. This runs the library's
+multi-rank path (pack, exchange, unpack, global passes); only the RCCL call of
+exchange_candidates is replaced."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, cfg, out_q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.join(os.path.dirname(here),
+                                    "kubernetes-native-distributed-ai-job-scheduler_amd"))
+    import torch
+    import oracle_bind as ob
+    from kplace import _abi, synth
+    from kplace.engine import Placer
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def allgather(data: bytes) -> bytes:
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+        bufs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(bufs, t)
+        return b"".join(b.numpy().tobytes() for b in bufs)
+
+    no, J, N = cfg
+    w = synth.config(no, J, N)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[no])
+    with Placer(device=0, world_size=world, rank=rank, allgather=allgather) as pl:
+        g = pl.place(w, p)
+    t = torch.from_numpy(g["node"].astype(np.int64))
+    all_nodes = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(all_nodes, t)
+    same = all(torch.equal(all_nodes[0], x) for x in all_nodes)
+    if rank == 0:
+        ref = ob.place(ob.SnapshotBuf.from_workload(w), p, nthreads=4)
+        ok = same and all(np.array_equal(g[k], ref[k]) for k in ("node", "score", "status", "used"))
+        out_q.put((ok, g["rounds"], ref["rounds"], g["placed"], ref["placed"]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cfg", [(2, 3000, 300), (3, 8000, 640)])
+def test_sharded_gpu_solve_matches_oracle(oracle, cfg):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, cfg, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = q.get(timeout=240)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    ok, r1, r0, p1, p0 = res
+    assert ok, "sharded GPU placement differs from the oracle"
+    assert (r1, p1) == (r0, p0)
