@@ -131,8 +131,8 @@ static int ensure_units(kp_ctx *c, int32_t U, int32_t J) {
       KP_TRY(dalloc(&c->d.act, u));
       KP_TRY(dalloc(&c->d.cand, u * K));
       KP_TRY(dalloc(&c->d.xg_counts, (size_t)c->world));
-      KP_TRY(dalloc(&c->d.xg_send, u * (K + 1)));
-      KP_TRY(dalloc(&c->d.xg_recv, (size_t)c->world * u * (K + 1)));
+      KP_TRY(dalloc(&c->d.xg_send, 1 + u * (K + 1)));
+      KP_TRY(dalloc(&c->d.xg_recv, (size_t)c->world * (1 + u * (K + 1))));
     } else {
       c->d.act = c->d.act_local;
       c->d.cand = c->d.cand_local;
@@ -499,65 +499,35 @@ int kp_load_jobs(kp_ctx *c, int32_t J, const int64_t *req, const int32_t *prio,
 }
 
 // ---------------------------------------------------------------------------
-// all-gather through host memory with the caller's transport (kp_set_allgather)
-static int exchange_host(kp_ctx *c, int32_t A_local, int32_t K, int32_t *A_global) {
-  const int W = c->world;
-  std::vector<int32_t> counts(W);
-  if (c->allgather(c->allgather_user, &A_local, sizeof(int32_t), counts.data()) != 0)
-    return KP_ERCCL;
-  int32_t Umax = 0, tot = 0;
-  for (int r = 0; r < W; ++r) {
-    Umax = std::max(Umax, counts[r]);
-    tot += counts[r];
+// This rank's candidates -> every rank's, as fixed-size blocks
+// [count, (unit, K candidates) x B] (B: the same slot bound on every rank), so
+// the all-gather needs no host-known count: one collective per round and, over
+// RCCL, no host synchronisation. The host-staged transport (kp_set_allgather)
+// moves the same blocks through host memory.
+static int exchange_round(kp_ctx *c, int32_t B, int32_t K) {
+  const size_t per = 1 + (size_t)B * (K + 1);
+  KP_TRY(launch_pack_exchange(c, B, K));
+  if (c->nccl_comm) {
+    if (ncclAllGather(c->d.xg_send, c->d.xg_recv, per, ncclInt32,
+                      static_cast<ncclComm_t>(c->nccl_comm), c->stream) != ncclSuccess)
+      return KP_ERCCL;
+  } else {
+    try {
+      c->h_xg_send.resize(per);
+      c->h_xg_recv.resize(per * c->world);
+    } catch (const std::bad_alloc &) {
+      return KP_ENOMEM;
+    }
+    KP_HIP(hipMemcpyAsync(c->h_xg_send.data(), c->d.xg_send, sizeof(int32_t) * per,
+                          hipMemcpyDeviceToHost, c->stream));
+    KP_HIP(hipStreamSynchronize(c->stream));
+    if (c->allgather(c->allgather_user, c->h_xg_send.data(), sizeof(int32_t) * per,
+                     c->h_xg_recv.data()) != 0)
+      return KP_ERCCL;
+    KP_HIP(hipMemcpyAsync(c->d.xg_recv, c->h_xg_recv.data(), sizeof(int32_t) * per * c->world,
+                          hipMemcpyHostToDevice, c->stream));
   }
-  *A_global = tot;
-  if (tot == 0) return KP_OK;
-  const size_t per = (size_t)Umax * (K + 1);
-  try {
-    c->h_xg_send.resize(per);
-    c->h_xg_recv.resize(per * W);
-  } catch (const std::bad_alloc &) {
-    return KP_ENOMEM;
-  }
-  KP_TRY(launch_pack_exchange(c, A_local, K));
-  KP_HIP(hipMemcpyAsync(c->h_xg_send.data(), c->d.xg_send, sizeof(int32_t) * per,
-                        hipMemcpyDeviceToHost, c->stream));
-  KP_HIP(hipStreamSynchronize(c->stream));
-  if (c->allgather(c->allgather_user, c->h_xg_send.data(), sizeof(int32_t) * per,
-                   c->h_xg_recv.data()) != 0)
-    return KP_ERCCL;
-  KP_HIP(hipMemcpyAsync(c->d.xg_counts, counts.data(), sizeof(int32_t) * W,
-                        hipMemcpyHostToDevice, c->stream));
-  KP_HIP(hipMemcpyAsync(c->d.xg_recv, c->h_xg_recv.data(), sizeof(int32_t) * per * W,
-                        hipMemcpyHostToDevice, c->stream));
-  KP_TRY(launch_unpack_exchange(c, W, Umax, K));
-  KP_HIP(hipStreamSynchronize(c->stream));  // the host buffers are reused next round
-  return KP_OK;
-}
-
-static int exchange_candidates(kp_ctx *c, int32_t A_local, int32_t K, int32_t *A_global) {
-  if (!c->nccl_comm) return exchange_host(c, A_local, K, A_global);
-  ncclComm_t comm = static_cast<ncclComm_t>(c->nccl_comm);
-  c->pinned[0] = A_local;
-  KP_HIP(hipMemcpyAsync(c->d.counters, c->pinned, sizeof(int32_t), hipMemcpyHostToDevice,
-                        c->stream));
-  if (ncclAllGather(c->d.counters, c->d.xg_counts, 1, ncclInt32, comm, c->stream) != ncclSuccess)
-    return KP_ERCCL;
-  KP_HIP(hipMemcpyAsync(c->pinned + 16, c->d.xg_counts, sizeof(int32_t) * c->world,
-                        hipMemcpyDeviceToHost, c->stream));
-  KP_HIP(hipStreamSynchronize(c->stream));
-  int32_t Umax = 0, tot = 0;
-  for (int r = 0; r < c->world; ++r) {
-    Umax = std::max(Umax, c->pinned[16 + r]);
-    tot += c->pinned[16 + r];
-  }
-  *A_global = tot;
-  if (tot == 0) return KP_OK;
-  KP_TRY(launch_pack_exchange(c, A_local, K));
-  if (ncclAllGather(c->d.xg_send, c->d.xg_recv, (size_t)Umax * (K + 1), ncclInt32, comm,
-                    c->stream) != ncclSuccess)
-    return KP_ERCCL;
-  return launch_unpack_exchange(c, c->world, Umax, K);
+  return launch_unpack_exchange(c, c->world, B, K);
 }
 
 static double ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -678,18 +648,47 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     }
     (void)hipEventDestroy(evA);
   } else {
-    // multi-GPU: the candidate exchange needs every rank's count on the host
-    for (int32_t r = 0;; ++r) {
+    // Multi-GPU, device-driven like the single-GPU loop: the local and the
+    // global active counts stay on the device (counters[0] / counters[1]);
+    // grids and exchange blocks are sized by the previous round's global
+    // count, which every rank reads asynchronously (the same value on all
+    // ranks, so every rank calls the all-gather with the same size).
+    hipEvent_t evG;
+    KP_HIP(hipEventCreateWithFlags(&evG, hipEventDisableTiming));
+    int32_t *Al_h = c->pinned + 256, *G_h = c->pinned + 320;
+    int64_t Smax = 0;  // largest shard
+    for (int r = 0; r < c->world; ++r)
+      Smax = std::max<int64_t>(Smax, (int64_t)U * (r + 1) / c->world - (int64_t)U * r / c->world);
+    const bool chunked = std::min<int64_t>(shard, Smax) > rpc;
+    int64_t G_bound = U;
+    for (int32_t r = 0; G_bound > 0; ++r) {
       if (p->max_rounds > 0 && r >= p->max_rounds) break;
-      int32_t A_local = 0, A = 0;
-      KP_TRY(launch_active(c, c->u_lo, c->u_hi, &A_local));
-      for (int64_t r0 = 0; r0 < A_local; r0 += rpc)
-        KP_TRY(score_select(r0, (int32_t)std::min<int64_t>(rpc, A_local - r0), nullptr, r));
-      round_active.push_back(A_local);
-      KP_TRY(exchange_candidates(c, A_local, K, &A));
-      if (A == 0) break;
-      KP_TRY(passes_of_round(A, nullptr));
+      const int32_t B = (int32_t)std::min<int64_t>(Smax, G_bound);  // per-rank slot bound
+      if (shard > 0) {
+        KP_TRY(launch_active_async(c, c->u_lo, c->u_hi, Al_h));
+      } else {  // an empty shard (fewer units than ranks) still joins the exchange
+        KP_HIP(hipMemsetAsync(c->d.counters, 0, sizeof(int32_t), c->stream));
+        *Al_h = 0;
+      }
+      const int32_t rows = (int32_t)std::min<int64_t>(shard, B);
+      if (chunked) {  // the score matrix is chunked: needs the exact local count
+        KP_HIP(hipStreamSynchronize(c->stream));
+        for (int64_t r0 = 0; r0 < *Al_h; r0 += rpc)
+          KP_TRY(score_select(r0, (int32_t)std::min<int64_t>(rpc, *Al_h - r0), nullptr, r));
+      } else if (rows > 0) {
+        KP_TRY(score_select(0, rows, c->d.counters, r));
+      }
+      KP_TRY(exchange_round(c, B, K));
+      KP_HIP(hipMemcpyAsync(G_h, c->d.counters + 1, sizeof(int32_t), hipMemcpyDeviceToHost,
+                            c->stream));
+      KP_HIP(hipEventRecord(evG, c->stream));
+      KP_TRY(passes_of_round((int32_t)std::min<int64_t>(U, (int64_t)B * c->world),
+                             c->d.counters + 1));
+      KP_HIP(hipEventSynchronize(evG));  // lands before this round's passes run
+      round_active.push_back(*Al_h);
+      G_bound = *G_h;
     }
+    (void)hipEventDestroy(evG);
   }
   KP_TRY(launch_finalize(c));
   KP_HIP(hipEventRecord(t1, c->stream));

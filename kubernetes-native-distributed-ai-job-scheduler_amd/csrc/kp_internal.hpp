@@ -183,8 +183,11 @@ int launch_accept(kp_ctx *c, const ScoreParams &sp, int32_t pass, int32_t A);
 int launch_active(kp_ctx *c, int32_t lo, int32_t hi, int32_t *A_host);
 int launch_reset_units(kp_ctx *c);
 int launch_finalize(kp_ctx *c);
-int launch_pack_exchange(kp_ctx *c, int32_t A, int32_t K);
-int launch_unpack_exchange(kp_ctx *c, int32_t world, int32_t Umax, int32_t K);
+// multi-GPU exchange blocks: [count, (unit, K candidates) x B] per rank; pack
+// reads the device count counters[0], unpack writes the global count to
+// counters[1]
+int launch_pack_exchange(kp_ctx *c, int32_t B, int32_t K);
+int launch_unpack_exchange(kp_ctx *c, int32_t world, int32_t B, int32_t K);
 size_t rocprim_temp_bytes(int32_t max_items);
 int launch_preempt(kp_ctx *c, int32_t *P_host);
 int launch_delta(kp_ctx *c, int32_t K, int32_t *bad_host);

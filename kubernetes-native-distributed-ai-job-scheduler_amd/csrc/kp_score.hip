@@ -659,27 +659,41 @@ __global__ void k_finalize(const int32_t *__restrict__ status, const int32_t *__
 }
 
 
-__global__ void k_unpack(int32_t world, int32_t Umax, int32_t K,
-                         const int32_t *__restrict__ counts, const int32_t *__restrict__ recv,
-                         int32_t *__restrict__ act, int32_t *__restrict__ cand) {
-  // one thread per (rank, local slot); destination = prefix of counts
+// Candidate exchange blocks (multi-GPU): per rank a fixed-size
+// block [count, (unit, K candidates) x B] so that every rank calls the same
+// all-gather without knowing the counts on the host.
+__global__ void k_pack(int32_t B, int32_t K, const int32_t *__restrict__ count,
+                       const int32_t *__restrict__ act, const int32_t *__restrict__ cand,
+                       int32_t *__restrict__ send) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int r = (int)(t / Umax), i = (int)(t % Umax);
-  if (r >= world || i >= counts[r]) return;
-  int32_t dst = i;
-  for (int k = 0; k < r; ++k) dst += counts[k];
-  const int32_t *src = recv + ((int64_t)r * Umax + i) * (K + 1);
-  act[dst] = src[0];
-  for (int k = 0; k < K; ++k) cand[(int64_t)dst * K + k] = src[1 + k];
-}
-
-__global__ void k_pack(int32_t A, int32_t K, const int32_t *__restrict__ act,
-                       const int32_t *__restrict__ cand, int32_t *__restrict__ send) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int32_t A = min(B, *count);
+  if (t == 0) send[0] = A;
   if (t >= A) return;
-  int32_t *dst = send + t * (K + 1);
+  int32_t *dst = send + 1 + t * (K + 1);
   dst[0] = act[t];
   for (int k = 0; k < K; ++k) dst[1 + k] = cand[t * K + k];
+}
+
+// every rank's block -> the global (unit, candidates) list in rank order (=
+// unit rank order: shards are contiguous) and its length in *total
+__global__ void k_unpack(int32_t world, int32_t B, int32_t K, const int32_t *__restrict__ recv,
+                         int32_t *__restrict__ act, int32_t *__restrict__ cand,
+                         int32_t *__restrict__ total) {
+  const int64_t per = 1 + (int64_t)B * (K + 1);
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int r = (int)(t / B), i = (int)(t % B);
+  if (r >= world) return;
+  int32_t dst = i, tot = 0;
+  for (int k = 0; k < world; ++k) {
+    const int32_t ck = recv[k * per];
+    if (k < r) dst += ck;
+    tot += ck;
+  }
+  if (t == 0) *total = tot;
+  if (i >= recv[r * per]) return;
+  const int32_t *src = recv + r * per + 1 + (int64_t)i * (K + 1);
+  act[dst] = src[0];
+  for (int k = 0; k < K; ++k) cand[(int64_t)dst * K + k] = src[1 + k];
 }
 
 // streaming churn: used[d][node[k]] += sign * delta[d*K + k] (int64 atomics,
@@ -915,18 +929,17 @@ int launch_finalize(kp_ctx *c) {
   return KP_OK;
 }
 
-int launch_unpack_exchange(kp_ctx *c, int32_t world, int32_t Umax, int32_t K) {
-  if (Umax <= 0) return KP_OK;
-  hipLaunchKernelGGL(k_unpack, dim3(blocks((int64_t)world * Umax, 256)), dim3(256), 0, c->stream,
-                     world, Umax, K, c->d.xg_counts, c->d.xg_recv, c->d.act, c->d.cand);
+int launch_unpack_exchange(kp_ctx *c, int32_t world, int32_t B, int32_t K) {
+  if (B <= 0) return KP_OK;
+  hipLaunchKernelGGL(k_unpack, dim3(blocks((int64_t)world * B, 256)), dim3(256), 0, c->stream,
+                     world, B, K, c->d.xg_recv, c->d.act, c->d.cand, c->d.counters + 1);
   KP_HIP(hipGetLastError());
   return KP_OK;
 }
 
-int launch_pack_exchange(kp_ctx *c, int32_t A, int32_t K) {
-  if (A <= 0) return KP_OK;
-  hipLaunchKernelGGL(k_pack, dim3(blocks(A, 256)), dim3(256), 0, c->stream, A, K,
-                     c->d.act_local, c->d.cand_local, c->d.xg_send);
+int launch_pack_exchange(kp_ctx *c, int32_t B, int32_t K) {
+  hipLaunchKernelGGL(k_pack, dim3(blocks(std::max(B, 1), 256)), dim3(256), 0, c->stream, B, K,
+                     c->d.counters, c->d.act_local, c->d.cand_local, c->d.xg_send);
   KP_HIP(hipGetLastError());
   return KP_OK;
 }

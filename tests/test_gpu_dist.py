@@ -24,7 +24,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, cfg, out_q):
+def _worker(rank, world, port, cfg, mpm, out_q):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, here)
@@ -47,7 +47,8 @@ def _worker(rank, world, port, cfg, out_q):
     no, J, N = cfg
     w = synth.config(no, J, N)
     p = _abi.default_params(**synth.CONFIG_PARAMS[no])
-    with Placer(device=0, world_size=world, rank=rank, allgather=allgather) as pl:
+    with Placer(device=0, world_size=world, rank=rank, allgather=allgather,
+                max_pairs_matrix=mpm) as pl:
         g = pl.place(w, p)
     t = torch.from_numpy(g["node"].astype(np.int64))
     all_nodes = [torch.empty_like(t) for _ in range(world)]
@@ -61,12 +62,18 @@ def _worker(rank, world, port, cfg, out_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("cfg", [(2, 3000, 300), (3, 8000, 640)])
-def test_sharded_gpu_solve_matches_oracle(oracle, cfg):
+@pytest.mark.parametrize("world,cfg,mpm", [
+    (2, (2, 3000, 300), 0),
+    (2, (3, 8000, 640), 0),
+    (2, (3, 1, 64), 0),            # rank 0 holds no unit
+    (3, (3, 6000, 512), 0),        # uneven shards
+    (2, (3, 6000, 512), 512 * 700),  # chunked score matrix (exact local count path)
+])
+def test_sharded_gpu_solve_matches_oracle(oracle, world, cfg, mpm):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, cfg, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cfg, mpm, q)) for r in range(world)]
     for pr in procs:
         pr.start()
     res = q.get(timeout=240)
