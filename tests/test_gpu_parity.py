@@ -76,6 +76,51 @@ def test_score_matrix_parity(oracle, placer, mode, scale):
     assert np.array_equal(sc >= 0, np.unpackbits(mk.view(np.uint8), axis=1, bitorder="little")[:, :w.N] == 1)
 
 
+def wide_workload(seed, J, N, D=4, top=32):
+    """Caps and requests across the 32-bit range (top = log2 bound): per dim
+    some waves hold only caps < 2^24 (full-rate 24-bit multiply), some caps up
+    to 2^top (quarter-rate path), some tiny caps <= S (the R-hi term); gangs of
+    up to 8 members so member-count products exceed 2^32 when top = 32."""
+    rng = np.random.default_rng(seed)
+    hi = np.int64(1) << np.int64(top)
+    cap = np.empty((D, N), np.int64)
+    for d in range(D):
+        kind = rng.integers(0, 3, size=N)
+        cap[d] = np.where(kind == 0, rng.integers(0, 100, size=N),
+                          np.where(kind == 1, rng.integers(1 << 20, 1 << 24, size=N),
+                                   rng.integers(1 << 24, hi, size=N)))
+        cap[d, :N // 3] = rng.integers(1 << 10, 1 << 23, size=N // 3)  # whole fast-24 waves
+    used = (cap * rng.random((D, N)) * 0.4).astype(np.int64)
+    w = random_workload(seed, J, N, D=D)
+    scale = rng.choice([1, 1 << 8, 1 << 16, 1 << 22], size=(D, 1))
+    req = np.minimum(w.req * scale, hi - 1)
+    # identical requests within a gang (random_workload's CR structure)
+    return synth.Workload(J, N, D, np.ascontiguousarray(req), cap, used, w.prio, w.gang_id,
+                          w.gang_size, w.topo, name=f"wide{seed}")
+
+
+@pytest.mark.parametrize("top", [31, 32])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_score_matrix_wide_32bit(oracle, placer, top, mode):
+    w = wide_workload(40 + top + mode, J=200, N=1500, top=top)
+    p = _abi.default_params(score_mode=mode)
+    placer.load_nodes(w.cap, w.used, w.topo)
+    placer.load_jobs(w.req)
+    sc, mk = placer.score(p, 0, w.J)
+    osc, omk = oracle.score(oracle.SnapshotBuf(w.req, w.cap, w.used, topo=w.topo), p, 0, w.J)
+    assert np.array_equal(sc, osc) and np.array_equal(mk, omk)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_place_wide_32bit_parity(oracle, placer, seed):
+    # full placements on the 32-bit score / plan paths with wide values
+    w = wide_workload(seed, J=1500, N=400, top=31 + seed % 2)
+    assert int(w.cap.max()) < (1 << 32) and int(w.req.max()) < (1 << 32)
+    p = _abi.default_params(score_mode=seed % 2, util_scale=[100, 1024, 7, 100][seed])
+    g, o = _place_both(oracle, placer, w, p)
+    _assert_same(g, o, f"wide seed {seed}")
+
+
 @pytest.mark.parametrize("D", [1, 2, 3, 5, 8])
 def test_score_matrix_dims(oracle, placer, D):
     w = random_workload(100 + D, J=130, N=200, D=D, gangs=False)
