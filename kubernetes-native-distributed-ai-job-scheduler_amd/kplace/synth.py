@@ -244,7 +244,8 @@ CONFIG_PARAMS = {
     3: dict(w_dim=(1, 1, 4, 2), w_gpu_fit=1024, w_spread=256),
     1: dict(w_dim=(1, 1, 4, 2), w_gpu_fit=1024, w_spread=256),
     4: dict(w_dim=(1, 1, 4, 2), w_gpu_fit=1024, w_spread=0),
-    5: dict(w_dim=(1, 1, 4, 2), w_gpu_fit=1024, w_spread=0),
+    # streaming: 32 candidates per unit (13 vs 22 rounds per 5k batch in steady state)
+    5: dict(w_dim=(1, 1, 4, 2), w_gpu_fit=1024, w_spread=0, n_cand=32),
 }
 
 
