@@ -176,7 +176,7 @@ def main():
             k = [v for n, v in json.load(f)["kernels"].items() if n.startswith("k_score")]
         if k:
             traffic = k[0]["traffic_bytes_per_launch"]
-            traffic_src = "profiles/r01_pmc.json (FETCH_SIZE x2 + WRITE_SIZE, tools/gpu_pmc.sh)"
+            traffic_src = "profiles/r01_pmc.json (FETCH_SIZE x2 + WRITE_SIZE, tools/gpu_evidence.sh)"
     out = {
         "metric": METRIC,
         "value": pairs / (ms / 1e3),
