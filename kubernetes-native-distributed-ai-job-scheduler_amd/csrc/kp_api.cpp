@@ -278,6 +278,7 @@ int kp_create(kp_ctx **out, const kp_config *cfg) {
   c->max_pairs_matrix = cfg->max_pairs_matrix;
   if (const char *e = std::getenv("KP_SELECT_LDS_CAP")) c->select_lds_cap = std::atoi(e);
   if (const char *e = std::getenv("KP_SELECT_GENERIC")) c->select_generic = std::atoi(e) != 0;
+  if (const char *e = std::getenv("KP_SELECT_BS")) c->select_bs = std::atoi(e);
   if (const char *e = std::getenv("KP_SCORE_WG_TARGET")) c->score_wg_target = std::max(64, std::atoi(e));
   if (const char *e = std::getenv("KP_SCORE_MIN_RPB")) c->score_min_rpb = std::max(1, std::atoi(e));
   if (const char *e = std::getenv("KP_SCORE_NPL")) c->score_npl = std::atoi(e) == 4 ? 4 : 2;

@@ -131,6 +131,7 @@ struct kp_ctx {
   // generic per-lane top-K select
   int32_t select_lds_cap = 0;
   bool select_generic = false;
+  int32_t select_bs = 0;  // KP_SELECT_BS: preferred threshold-select block size
   // score launch geometry (tuning knobs): target workgroups per launch and
   // the smallest number of job rows per workgroup
   int32_t score_wg_target = 2048, score_min_rpb = 4, score_npl = 2;

@@ -46,6 +46,19 @@ __global__ void k_prep_nodes(const int64_t *__restrict__ cap, uint64_t *__restri
 // straight into the row's mask words.
 // Row stride of score/mask = Ns = round_up(N, 64); padding is infeasible.
 // ---------------------------------------------------------------------------
+// The grid of a device-driven round is sized by a bound on its rows (the
+// previous round's count); the actual count (*rows_dev) is spread over every
+// launched row block, at least min_rpb rows each, so a shrunken round still
+// fills the chip instead of leaving most blocks idle and the rest long.
+// rows_per_block only shrinks (the LDS request stage stays in bounds) and
+// gridDim.y * rpb >= rows holds either way.
+__device__ __forceinline__ void fit_rows(int32_t act, int32_t min_rpb, int32_t &rows,
+                                         int32_t &rows_per_block) {
+  rows = min(rows, act);
+  const int32_t even = (rows + (int32_t)gridDim.y - 1) / (int32_t)gridDim.y;
+  rows_per_block = min(rows_per_block, max(min_rpb, even));
+}
+
 template <int D, int NPL>
 __global__ __launch_bounds__(256) void k_score(ScoreParams sp,
                                                const int64_t *__restrict__ cap,
@@ -55,10 +68,10 @@ __global__ __launch_bounds__(256) void k_score(ScoreParams sp,
                                                const int64_t *__restrict__ q, int32_t qstride,
                                                const int32_t *__restrict__ rows_unit,
                                                int32_t rows, int32_t rows_per_block,
-                                               int32_t *__restrict__ score,
+                                               int32_t min_rpb, int32_t *__restrict__ score,
                                                uint64_t *__restrict__ mask, int32_t Ns,
                                                const int32_t *__restrict__ rows_dev) {
-  if (rows_dev) rows = min(rows, *rows_dev);
+  if (rows_dev) fit_rows(*rows_dev, min_rpb, rows, rows_per_block);
   if ((int)blockIdx.y * rows_per_block >= rows) return;  // block-uniform
   const int N = sp.N;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -216,12 +229,12 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
                                                  const int64_t *__restrict__ q, int32_t qstride,
                                                  const int32_t *__restrict__ rows_unit,
                                                  int32_t rows, int32_t rows_per_block,
-                                                 int32_t *__restrict__ score,
+                                                 int32_t min_rpb, int32_t *__restrict__ score,
                                                  uint64_t *__restrict__ mask, int32_t Ns,
                                                  const int32_t *__restrict__ rows_dev) {
   static_assert(NPL == 2 || NPL == 4, "2 or 4 nodes per lane");
   using V = Vec<NPL>;
-  if (rows_dev) rows = min(rows, *rows_dev);
+  if (rows_dev) fit_rows(*rows_dev, min_rpb, rows, rows_per_block);
   if ((int)blockIdx.y * rows_per_block >= rows) return;  // block-uniform
   __shared__ uint32_t sq[kScoreMaxRows][D + 1];  // [D] = request in the GPU dim (0 if none)
   const int N = sp.N;
@@ -741,7 +754,7 @@ struct ScoreL {
       dim3 grid(tiles, blocks(rows, rpb));
 #define KP_SC32(M, NP)                                                                      \
   hipLaunchKernelGGL((k_score32<D, M, NP>), grid, dim3(256), 0, c->stream, sp, c->d.np32, P, q, \
-                     qstride, rows_unit, rows, rpb, score, mask, Ns, rows_dev)
+                     qstride, rows_unit, rows, rpb, c->score_min_rpb, score, mask, Ns, rows_dev)
       if (sp.most_allocated) {
         if (npl == 4) KP_SC32(true, 4); else KP_SC32(true, 2);
       } else {
@@ -753,8 +766,8 @@ struct ScoreL {
       const int rpb = 32;
       dim3 grid(blocks(Ns, 256 * NPL), blocks(rows, rpb));
       hipLaunchKernelGGL((k_score<D, NPL>), grid, dim3(256), 0, c->stream, sp, c->d.cap,
-                         c->d.used, c->d.R, c->d.base, q, qstride, rows_unit, rows, rpb, score,
-                         mask, Ns, rows_dev);
+                         c->d.used, c->d.R, c->d.base, q, qstride, rows_unit, rows, rpb,
+                         c->score_min_rpb, score, mask, Ns, rows_dev);
     }
     KP_HIP(hipGetLastError());
     return KP_OK;
@@ -783,6 +796,45 @@ int launch_score(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int
   return dispatch_D<ScoreL>(c->D, c, sp, rows_unit, rows, score, mask, q, qstride, rows_dev);
 }
 
+// Threshold-select shapes (V4 16-B loads per thread x BS threads cover
+// 4*V4*BS nodes of a row). Per row width the first listed shape of the
+// preferred block size that covers the row: few row entries per thread keeps
+// the row in fewer VGPRs (more resident waves, more loads in flight).
+namespace {
+using SelFn = void (*)(dim3, hipStream_t, const ScoreParams &, const int32_t *, int32_t,
+                       const int32_t *, const uint32_t *, int32_t, int32_t, int32_t *,
+                       const int32_t *);
+template <int V4, int BS>
+void sel_t(dim3 grid, hipStream_t st, const ScoreParams &sp, const int32_t *score, int32_t Ns,
+           const int32_t *rows_unit, const uint32_t *salt, int32_t rows, int32_t cap,
+           int32_t *cand, const int32_t *rows_dev) {
+  hipLaunchKernelGGL((k_select_t<V4, BS>), grid, dim3(BS), 0, st, sp, score, Ns, rows_unit, salt,
+                     rows, cap, cand, rows_dev);
+}
+struct SelShape {
+  int v4, bs;
+  SelFn fn;
+};
+const SelShape kSelShapes[] = {
+    {1, 256, sel_t<1, 256>},    {2, 256, sel_t<2, 256>},    {3, 256, sel_t<3, 256>},
+    {4, 256, sel_t<4, 256>},    {6, 256, sel_t<6, 256>},    {8, 256, sel_t<8, 256>},
+    {12, 256, sel_t<12, 256>},  {16, 256, sel_t<16, 256>},  {2, 512, sel_t<2, 512>},
+    {3, 512, sel_t<3, 512>},    {4, 512, sel_t<4, 512>},    {5, 512, sel_t<5, 512>},
+    {6, 512, sel_t<6, 512>},    {8, 512, sel_t<8, 512>},    {4, 1024, sel_t<4, 1024>},
+    {5, 1024, sel_t<5, 1024>},  {6, 1024, sel_t<6, 1024>},  {8, 1024, sel_t<8, 1024>},
+    {10, 1024, sel_t<10, 1024>}, {17, 768, sel_t<17, 768>},
+};
+const SelShape *sel_shape(int Ns, int pref_bs) {
+  const SelShape *best = nullptr;
+  for (const SelShape &s : kSelShapes) {
+    if (4 * s.v4 * s.bs < Ns) continue;
+    if (pref_bs > 0 && s.bs != pref_bs) continue;
+    if (!best) best = &s;
+  }
+  return best;
+}
+}  // namespace
+
 int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
                   const int32_t *score, int32_t *cand, const int32_t *rows_dev) {
   if (rows <= 0) return KP_OK;
@@ -790,40 +842,32 @@ int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, in
   const int K = sp.n_cand;
   const int lim = c->select_lds_cap > 0 ? std::min(c->select_lds_cap, kSelLdsCap) : kSelLdsCap;
   const int cap = std::max(K + 1, lim);
-  const bool generic = c->select_generic || Ns > 3072 * 17;
   dim3 grid(rows);
-#define KP_SEL_T(V4, BS)                                                                 \
-  hipLaunchKernelGGL((k_select_t<V4, BS>), grid, dim3(BS), 0, c->stream, sp, score, Ns,  \
-                     rows_unit, c->d.salt, rows, cap, cand, rows_dev)
-  if (generic) {
-    if (K <= 4)
-      hipLaunchKernelGGL(k_select<4>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
-                         c->d.salt, rows, cand, rows_dev);
-    else if (K <= 8)
-      hipLaunchKernelGGL(k_select<8>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
-                         c->d.salt, rows, cand, rows_dev);
-    else if (K <= 16)
-      hipLaunchKernelGGL(k_select<16>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
-                         c->d.salt, rows, cand, rows_dev);
-    else
-      hipLaunchKernelGGL(k_select<32>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
-                         c->d.salt, rows, cand, rows_dev);
-  } else if (Ns <= 1024 * 1) {
-    KP_SEL_T(1, 256);
-  } else if (Ns <= 1024 * 2) {
-    KP_SEL_T(2, 256);
-  } else if (Ns <= 1024 * 4) {
-    KP_SEL_T(4, 256);
-  } else if (Ns <= 1024 * 8) {
-    KP_SEL_T(8, 256);
-  } else if (Ns <= 1024 * 16) {
-    KP_SEL_T(16, 256);
-  } else if (Ns <= 4096 * 8) {
-    KP_SEL_T(8, 1024);
+  // preferred block size: 256 threads up to 4k nodes, 512 up to 16k, 1024
+  // up to 40k (at most 128 VGPRs per thread), else 768 (KP_SELECT_BS overrides); rows wider than every
+  // shape: generic form
+  const int pref = c->select_bs > 0 ? c->select_bs
+                   : Ns <= 4096     ? 256
+                   : Ns <= 16384    ? 512
+                   : Ns <= 40960    ? 1024
+                                    : 768;
+  const SelShape *sh = c->select_generic ? nullptr : sel_shape(Ns, pref);
+  if (!sh && !c->select_generic) sh = sel_shape(Ns, 0);
+  if (sh) {
+    sh->fn(grid, c->stream, sp, score, Ns, rows_unit, c->d.salt, rows, cap, cand, rows_dev);
+  } else if (K <= 4) {
+    hipLaunchKernelGGL(k_select<4>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
+                       c->d.salt, rows, cand, rows_dev);
+  } else if (K <= 8) {
+    hipLaunchKernelGGL(k_select<8>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
+                       c->d.salt, rows, cand, rows_dev);
+  } else if (K <= 16) {
+    hipLaunchKernelGGL(k_select<16>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
+                       c->d.salt, rows, cand, rows_dev);
   } else {
-    KP_SEL_T(17, 768);  // 12 waves (3 per SIMD, up to 168 VGPRs): no spill
+    hipLaunchKernelGGL(k_select<32>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
+                       c->d.salt, rows, cand, rows_dev);
   }
-#undef KP_SEL_T
   KP_HIP(hipGetLastError());
   return KP_OK;
 }
