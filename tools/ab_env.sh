@@ -1,0 +1,13 @@
+# A/B timing of one library-tuning environment knob in ONE GPU call:
+#   bash tools/ab_env.sh KP_ACC_WAVES "0 1024 4096"
+# every value is run alternately, 3 times each, bench without events.
+set -o pipefail
+VAR=$1; VALS=$2
+mkdir -p gpurun_out/ab
+for i in 1 2 3; do
+  for v in $VALS; do
+    n=${VAR}_$v
+    env $VAR=$v timeout -k 10 120 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-stream --no-kernel-events --out gpurun_out/ab/$n.$i.json > gpurun_out/ab/$n.$i.log 2>&1 || exit $?
+    python3 -c "import json;b=json.load(open('gpurun_out/ab/$n.$i.json'));print('$n', round(b['ms_per_step'],3), b['config']['rounds'], b['config']['passes'], b['config']['placed_jobs'])"
+  done
+done
