@@ -197,6 +197,25 @@ def test_select_paths_parity(oracle, monkeypatch, knob, n_cand, tie):
     _assert_same(g, o, f"{knob} K={n_cand}")
 
 
+@pytest.mark.parametrize("knobs", [
+    (("KP_SCORE_WG_TARGET", "64"),),                                 # 128 rows per workgroup
+    (("KP_SCORE_WG_TARGET", "1000000"), ("KP_SCORE_MIN_RPB", "1")),  # one row per workgroup
+    (("KP_SCORE_NPL", "4"),),                                        # 4 nodes per lane
+    (("KP_SCORE_NPL", "4"), ("KP_SCORE_MIN_RPB", "3")),              # ragged last row block
+])
+def test_score_geometry_parity(oracle, monkeypatch, knobs):
+    """Every filter+score launch geometry (rows per workgroup, nodes per lane)
+    gives the oracle's placement; N = 1,500 leaves a partial node tile."""
+    for k, v in knobs:
+        monkeypatch.setenv(k, v)
+    w = synth.config3(7_000, 1_500)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[3])
+    with Placer(device=0) as pl:
+        g = pl.place(w, p)
+    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
+    _assert_same(g, o, f"score geometry {knobs}")
+
+
 def test_place_wide_rows_parity(oracle, placer):
     """Rows above 16384 nodes take the 1024-thread select form."""
     w = synth.config2(3_000, 20_000)
