@@ -593,9 +593,26 @@ struct AcceptL {
 
 }  // namespace
 
+// CSR sort configuration: rounds with up to KP_SORT_SINGLE_BS x KP_SORT_SINGLE_IPT
+// entries sort in one workgroup (rocprim's default: 1,024); larger ones run the
+// block sort + merge passes on tiles of KP_SORT_TILE_BS x KP_SORT_TILE_IPT
+// entries. 8,192 / 4,096: rocprim kernels 3.63 -> 3.21 ms per config #3 solve
+// (rocprofv3; 8,192-entry tiles: 3.42 ms, 4,096 / 4,096: 3.24 ms).
+#ifndef KP_SORT_SINGLE_BS
+#define KP_SORT_SINGLE_BS 1024
+#define KP_SORT_SINGLE_IPT 8
+#endif
+#ifndef KP_SORT_TILE_BS
+#define KP_SORT_TILE_BS 1024
+#define KP_SORT_TILE_IPT 4
+#endif
+using CsrMergeCfg = rocprim::merge_sort_config<512, KP_SORT_TILE_BS, KP_SORT_TILE_IPT>;
+using CsrSortCfg = rocprim::radix_sort_config<
+    rocprim::kernel_config<KP_SORT_SINGLE_BS, KP_SORT_SINGLE_IPT>, CsrMergeCfg>;
+
 size_t rocprim_temp_bytes(int32_t max_items) {
   size_t a = 0, s = 0;
-  (void)rocprim::radix_sort_pairs(nullptr, a, (uint32_t *)nullptr, (uint32_t *)nullptr,
+  (void)rocprim::radix_sort_pairs<CsrSortCfg>(nullptr, a, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                   (uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)max_items,
                                   0u, 32u);
   (void)rocprim::select(nullptr, s, rocprim::counting_iterator<int32_t>(0), (int32_t *)nullptr,
@@ -616,7 +633,7 @@ int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev) {
   unsigned bits = 1;
   while ((1ll << bits) <= c->N) ++bits;  // key N (invalid) must fit too
   size_t tb = c->d.temp_bytes;
-  KP_HIP(rocprim::radix_sort_pairs(c->d.temp, tb, c->d.csr_kin, c->d.csr_keys, c->d.csr_vin,
+  KP_HIP(rocprim::radix_sort_pairs<CsrSortCfg>(c->d.temp, tb, c->d.csr_kin, c->d.csr_keys, c->d.csr_vin,
                                    c->d.csr_vals, (size_t)P, 0u, bits, c->stream));
   hipLaunchKernelGGL(k_csr_finish, dim3(blocks(P, 256)), dim3(256), 0, c->stream, (int32_t)P,
                      c->N, K, c->D, c->U, c->d.csr_keys, c->d.csr_vals, c->d.act, c->d.q,
