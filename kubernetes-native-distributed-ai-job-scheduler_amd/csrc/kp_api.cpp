@@ -282,6 +282,7 @@ int kp_create(kp_ctx **out, const kp_config *cfg) {
   if (const char *e = std::getenv("KP_SCORE_WG_TARGET")) c->score_wg_target = std::max(64, std::atoi(e));
   if (const char *e = std::getenv("KP_SCORE_MIN_RPB")) c->score_min_rpb = std::max(1, std::atoi(e));
   if (const char *e = std::getenv("KP_SCORE_NPL")) c->score_npl = std::atoi(e) == 4 ? 4 : 2;
+  if (const char *e = std::getenv("KP_COMPACT_MAX")) c->compact_max = std::atoi(e);
   if (hipSetDevice(dev) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void **>(&c->pinned), 4096, hipHostMallocDefault) !=

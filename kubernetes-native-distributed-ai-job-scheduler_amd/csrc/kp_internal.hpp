@@ -135,6 +135,8 @@ struct kp_ctx {
   // score launch geometry (tuning knobs): target workgroups per launch and
   // the smallest number of job rows per workgroup
   int32_t score_wg_target = 4096, score_min_rpb = 4, score_npl = 2;
+  // KP_COMPACT_MAX: largest unit range compacted by the one-workgroup kernel
+  int32_t compact_max = 262144;
   // sizes
   int32_t N = 0, D = 0, J = 0, U = 0, R = 0, cap_R = 0, cap_delta = 0;
   int32_t cap_N = 0, cap_U = 0, cap_J = 0, cap_rows = 0, cap_props = 0, cap_K = 0;

@@ -734,6 +734,61 @@ __global__ void k_delta_check(int32_t K, int32_t N, int32_t D, const int32_t *__
   if (u < 0 || u > cap[i]) *bad = 1;
 }
 
+// Order-preserving compaction of the active-unit flags in ONE workgroup:
+// out = [lo + i for i in [0, n) if flag[i]], *count = its length. Chunks of
+// 1024 threads x 16 flags (four 16-B loads per thread), block scan of the
+// thread counts, running carry between chunks. Replaces rocprim::select's
+// lookback-state init + partition launches (2 kernels, ~13 us per round) for
+// the round's few-ten-thousand units.
+constexpr int kCompactBS = 1024, kCompactIPT = 16;
+__global__ __launch_bounds__(kCompactBS) void k_compact(const int32_t *__restrict__ flag, int32_t n,
+                                                        int32_t lo, int32_t *__restrict__ out,
+                                                        int32_t *__restrict__ count) {
+  __shared__ int32_t wsum[kCompactBS / kWave];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int32_t carry = 0;
+  for (int32_t base = 0; base < n; base += kCompactBS * kCompactIPT) {
+    const int32_t i0 = base + t * kCompactIPT;
+    int32_t f[kCompactIPT];
+    if (i0 + kCompactIPT <= n) {  // flag is 16-B aligned (device allocation), i0 % 16 == 0
+      const int4 *p = reinterpret_cast<const int4 *>(flag + i0);
+#pragma unroll
+      for (int v = 0; v < kCompactIPT / 4; ++v) {
+        const int4 x = p[v];
+        f[4 * v] = x.x; f[4 * v + 1] = x.y; f[4 * v + 2] = x.z; f[4 * v + 3] = x.w;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kCompactIPT; ++k) f[k] = i0 + k < n ? flag[i0 + k] : 0;
+    }
+    int32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < kCompactIPT; ++k) c += f[k] != 0;
+    int32_t inc = c;  // wave inclusive scan
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const int32_t o = __shfl_up(inc, d, kWave);
+      if (lane >= d) inc += o;
+    }
+    if (lane == kWave - 1) wsum[w] = inc;
+    __syncthreads();
+    int32_t before = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < kCompactBS / kWave; ++k) {
+      const int32_t s = wsum[k];
+      before += k < w ? s : 0;
+      total += s;
+    }
+    int32_t pos = carry + before + inc - c;
+#pragma unroll
+    for (int k = 0; k < kCompactIPT; ++k)
+      if (f[k] != 0) out[pos++] = lo + i0 + k;
+    carry += total;
+    __syncthreads();  // wsum reused by the next chunk
+  }
+  if (t == 0) *count = carry;
+}
+
 template <int D>
 struct ScoreL {
   static int run(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
@@ -901,6 +956,20 @@ static int launch_round_start(kp_ctx *c, int32_t lo, int32_t hi, int32_t *flag) 
 
 int launch_pack(kp_ctx *c) { return launch_round_start(c, 0, 0, nullptr); }
 
+// flags[0, n) -> act_local (lo + index, rank order), count -> counters[0]; one
+// workgroup up to KP_COMPACT_MAX flags (default 262,144), rocprim::select above
+static int launch_compact(kp_ctx *c, const int32_t *flag, int32_t lo, int32_t n, size_t tb) {
+  if (n <= c->compact_max) {
+    hipLaunchKernelGGL(k_compact, dim3(1), dim3(kCompactBS), 0, c->stream, flag, n, lo,
+                       c->d.act_local, c->d.counters);
+    KP_HIP(hipGetLastError());
+    return KP_OK;
+  }
+  KP_HIP(rocprim::select(c->d.temp, tb, rocprim::counting_iterator<int32_t>(lo), flag,
+                         c->d.act_local, c->d.counters, (size_t)n, c->stream));
+  return KP_OK;
+}
+
 // active units of [lo, hi) in rank order -> act_local; count to host
 int launch_active(kp_ctx *c, int32_t lo, int32_t hi, int32_t *A_host) {
   *A_host = 0;
@@ -909,8 +978,7 @@ int launch_active(kp_ctx *c, int32_t lo, int32_t hi, int32_t *A_host) {
   int32_t *flag = c->d.flag;
   KP_TRY(launch_round_start(c, lo, hi, flag));
   size_t tb = c->d.temp_bytes;
-  KP_HIP(rocprim::select(c->d.temp, tb, rocprim::counting_iterator<int32_t>(lo), flag,
-                         c->d.act_local, c->d.counters, (size_t)n, c->stream));
+  KP_TRY(launch_compact(c, flag, lo, n, tb));
   KP_HIP(hipMemcpyAsync(c->pinned, c->d.counters, sizeof(int32_t), hipMemcpyDeviceToHost,
                         c->stream));
   KP_HIP(hipStreamSynchronize(c->stream));
@@ -948,8 +1016,7 @@ int launch_active_async(kp_ctx *c, int32_t lo, int32_t hi, int32_t *count_host) 
   if (n <= 0) return KP_EINVAL;
   KP_TRY(launch_round_start(c, lo, hi, c->d.flag));
   size_t tb = c->d.temp_bytes;
-  KP_HIP(rocprim::select(c->d.temp, tb, rocprim::counting_iterator<int32_t>(lo), c->d.flag,
-                         c->d.act_local, c->d.counters, (size_t)n, c->stream));
+  KP_TRY(launch_compact(c, c->d.flag, lo, n, tb));
   KP_HIP(hipMemcpyAsync(count_host, c->d.counters, sizeof(int32_t), hipMemcpyDeviceToHost,
                         c->stream));
   return KP_OK;

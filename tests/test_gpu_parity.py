@@ -216,6 +216,20 @@ def test_score_geometry_parity(oracle, monkeypatch, knobs):
     _assert_same(g, o, f"score geometry {knobs}")
 
 
+@pytest.mark.parametrize("cmax", ["0", "3000"])
+def test_active_compaction_paths_parity(oracle, monkeypatch, cmax):
+    """The rocprim::select fallback of the active-unit compaction (every round,
+    or only the large early rounds) gives the same placement as the
+    one-workgroup kernel and the oracle."""
+    monkeypatch.setenv("KP_COMPACT_MAX", cmax)
+    w = synth.config3(20_000, 1_000)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[3])
+    with Placer(device=0) as pl:
+        g = pl.place(w, p)
+    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
+    _assert_same(g, o, f"KP_COMPACT_MAX={cmax}")
+
+
 def test_place_wide_rows_parity(oracle, placer):
     """Rows above 16384 nodes take the 1024-thread select form."""
     w = synth.config2(3_000, 20_000)
