@@ -606,8 +606,8 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     return KP_OK;
   };
   auto passes_of_round = [&](int32_t A, const int32_t *A_dev) -> int {
-    KP_TRY(launch_open_init(c, A, K, A_dev));
-    KP_TRY(launch_csr_build(c, A, K, A_dev));  // also banks + clears the pass flags
+    // also opens the slots, banks + clears the pass flags
+    KP_TRY(launch_csr_build(c, A, K, A_dev));
     // passes run back to back on the device: no host round trip inside a round
     for (int32_t pass = 0; pass < p->max_passes; ++pass) {
       KP_TRY(launch_plan(c, sp, A, pass, A_dev));

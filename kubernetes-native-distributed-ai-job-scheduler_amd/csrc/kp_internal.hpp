@@ -177,7 +177,6 @@ int launch_score(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit,
 int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit,
                   int32_t rows, const int32_t *score, int32_t *cand,
                   const int32_t *rows_dev = nullptr);
-int launch_open_init(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev = nullptr);
 int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev = nullptr);
 int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass,
                 const int32_t *A_dev = nullptr);

@@ -37,16 +37,28 @@ constexpr uint32_t kNoBid = 0xFFFFFFFFu;  // tag that matches no pass
 
 // ---- inverse index (once per round) --------------------------------------------
 // Also re-initialises the round's pass state (bids, window flags, node
-// segments, pass flags) so no memset launch is needed.
+// segments, pass flags) so no memset launch is needed, and opens the round's
+// slots: a unit without a candidate is NO_FIT (the former k_open_init).
+// Counts the round in the device statistics.
 __global__ void k_csr_keys(int32_t A, int32_t K, int32_t N, int64_t nwin,
                            const int32_t *__restrict__ cand, uint32_t *__restrict__ keys,
                            uint32_t *__restrict__ vals, uint32_t *__restrict__ bid,
                            int32_t *__restrict__ win, int32_t *__restrict__ seg_start,
                            int32_t *__restrict__ pass_flag, int32_t *__restrict__ node_flag,
                            int32_t *__restrict__ nl_count, const int32_t *__restrict__ A_dev,
-                           SolveStats *__restrict__ st) {
+                           SolveStats *__restrict__ st, const int32_t *__restrict__ act,
+                           uint8_t *__restrict__ open, int32_t *__restrict__ status) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int32_t Aa = A_dev ? min(A, *A_dev) : A;  // slots past the device count: no bids
+  if (t == 0 && Aa > 0) {  // one writer: a round with active units
+    st->rounds += 1;
+    st->active_sum += Aa;
+  }
+  if (t < Aa) {
+    const bool has = cand[t * K] >= 0;
+    open[t] = has ? 1 : 0;
+    if (!has) status[act[t]] = kNoFit;
+  }
   if (t < (int64_t)A * K) {
     const int32_t n = t < (int64_t)Aa * K ? cand[t] : -1;
     const int32_t a = (int32_t)(t / K), c = (int32_t)(t % K);
@@ -627,7 +639,8 @@ int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev) {
   const int64_t n = std::max<int64_t>(std::max<int64_t>(P, c->N), std::max<int64_t>(nwin, 64));
   hipLaunchKernelGGL(k_csr_keys, dim3(blocks(n, 256)), dim3(256), 0, c->stream, A, K, c->N, nwin,
                      c->d.cand, c->d.csr_kin, c->d.csr_vin, c->d.bid, c->d.win, c->d.seg_start,
-                     c->d.pass_flag, c->d.node_flag, c->d.counters + 32, A_dev, c->d.stats);
+                     c->d.pass_flag, c->d.node_flag, c->d.counters + 32, A_dev, c->d.stats,
+                     c->d.act, c->d.open, c->d.status);
   KP_HIP(hipGetLastError());
   if (P == 0) return KP_OK;
   unsigned bits = 1;

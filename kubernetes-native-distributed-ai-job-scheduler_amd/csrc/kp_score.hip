@@ -620,22 +620,6 @@ __global__ __launch_bounds__(256) void k_select(ScoreParams sp,
 // ---------------------------------------------------------------------------
 // round bookkeeping
 // ---------------------------------------------------------------------------
-__global__ void k_open_init(const int32_t *__restrict__ act, const int32_t *__restrict__ cand,
-                            int32_t A, int32_t K, uint8_t *__restrict__ open,
-                            int32_t *__restrict__ status, const int32_t *__restrict__ A_dev,
-                            SolveStats *__restrict__ st) {
-  if (A_dev) A = min(A, *A_dev);
-  int a = blockIdx.x * blockDim.x + threadIdx.x;
-  if (a == 0 && A > 0) {  // one writer: a round with active units
-    st->rounds += 1;
-    st->active_sum += A;
-  }
-  if (a >= A) return;
-  const bool has = cand[(int64_t)a * K] >= 0;
-  open[a] = has ? 1 : 0;
-  if (!has) status[act[a]] = kNoFit;
-}
-
 __global__ void k_reset_units(int32_t *__restrict__ status, int32_t U,
                               int32_t *__restrict__ job_node, int32_t *__restrict__ job_score,
                               int32_t J) {
@@ -923,14 +907,6 @@ int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, in
     hipLaunchKernelGGL(k_select<32>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
                        c->d.salt, rows, cand, rows_dev);
   }
-  KP_HIP(hipGetLastError());
-  return KP_OK;
-}
-
-int launch_open_init(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev) {
-  if (A <= 0) return KP_OK;
-  hipLaunchKernelGGL(k_open_init, dim3(blocks(A, 256)), dim3(256), 0, c->stream, c->d.act,
-                     c->d.cand, A, K, c->d.open, c->d.status, A_dev, c->d.stats);
   KP_HIP(hipGetLastError());
   return KP_OK;
 }
