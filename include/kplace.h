@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 1
+#define KP_ABI_VERSION 2
 
 /* ---- limits ------------------------------------------------------------ */
 #define KP_MAX_DIMS 8       /* resource dimensions per job/node               */
@@ -84,6 +84,12 @@ typedef struct kp_snapshot {
   const int32_t *gang_id;      /* [J] <0 = singleton; NULL = all singletons   */
   const int32_t *gang_size;    /* [J] checked against the run length; NULL ok */
   const int32_t *topo_domain;  /* [N] >= 0 (rack / xGMI island); NULL = n     */
+  /* [J] topo domain this job prefers, -1 = none; NULL = all -1. The
+     CacheStrategy "shared" term (api/v1/llmservice_types.go:42-44): the
+     domain of the node running the CR's Status.CacheCoordinator (:60), so
+     replicas that fetch the model from the coordinator stay on its xGMI
+     island / rack (docs/PROJECT_ROADMAP.md:173-174). Equal within a gang. */
+  const int32_t *affinity;
 } kp_snapshot;
 
 /* Scoring / assignment knobs (manager flags in the Go host). */
@@ -102,6 +108,8 @@ typedef struct kp_params {
   int32_t util_scale;         /* per-dim utilisation scale S, 1..1024
                                  (100 = kube-scheduler MaxNodeScore)          */
   int32_t max_passes;         /* acceptance passes per round, 1..64           */
+  int32_t w_affinity;         /* bonus when the node's topo domain equals the
+                                 job's affinity domain, 0..2^20               */
 } kp_params;
 
 /* Fills *p with the documented defaults. */
@@ -136,8 +144,26 @@ typedef struct kp_config {
 } kp_config;
 
 int kp_create(kp_ctx **out, const kp_config *cfg);
+/*
+ * One context over n_gpus GPUs of this node, for a single manager process
+ * (cmd/manager/main.go:157-200 runs ONE process with one reconciler,
+ * :181-187): the library runs one worker thread per GPU, each owning a
+ * row shard of the pending units, and exchanges candidates
+ * over RCCL (communicators from ncclCommInitAll inside the library) when the
+ * ids are distinct, or through host memory when an id repeats (one GPU
+ * driving several shards: testing). Every other entry point accepts the
+ * returned context unchanged; outputs come from shard 0 (all shards commit
+ * identical placements). cfg: only max_pairs_matrix is read (may be NULL).
+ */
+int kp_create_multi(kp_ctx **out, const int32_t *gpu_ids, int32_t n_gpus,
+                    const kp_config *cfg);
 void kp_destroy(kp_ctx *ctx);
+/* Generic text of an error code (static storage). */
 const char *kp_strerror(int code);
+/* Detailed text of the last error returned on this context (the HIP/RCCL
+   call and its message), "" if none. Valid until the next call on ctx; safe
+   from any OS thread (kept per context, not per thread). */
+const char *kp_last_error(kp_ctx *ctx);
 int kp_abi_version(void);
 /* Writes the 128-byte RCCL unique id for a multi-process context. */
 int kp_dist_unique_id(void *out128);
@@ -151,8 +177,11 @@ typedef int (*kp_allgather_fn)(void *user, const void *send, size_t bytes, void 
 int kp_set_allgather(kp_ctx *ctx, kp_allgather_fn fn, void *user);
 
 /*
- * One-shot placement: validate + upload the snapshot, solve, download.
- * Synchronous. Replaces one kube-scheduler cycle per pending pod.
+ * One-shot placement: validate + upload the snapshot, solve, download, under
+ * ONE acquisition of the context lock (concurrent kp_place calls on one
+ * context never interleave their snapshots). Synchronous. Replaces one
+ * kube-scheduler cycle per pending pod. A failed load leaves the context
+ * with no snapshot loaded (later kp_solve/kp_fetch return KP_ESTATE).
  */
 int kp_place(kp_ctx *ctx, const kp_snapshot *s, const kp_params *p,
              kp_result *r);
@@ -164,7 +193,7 @@ int kp_load_nodes(kp_ctx *ctx, int32_t N, int32_t D, const int64_t *cap,
 /* Upload (validate, group into gangs, rank) the pending queue. */
 int kp_load_jobs(kp_ctx *ctx, int32_t J, const int64_t *req,
                  const int32_t *prio, const int32_t *gang_id,
-                 const int32_t *gang_size);
+                 const int32_t *gang_size, const int32_t *affinity);
 /* Solve the loaded queue against the resident node table and commit the
    accepted placements into it. Inputs must already be resident. */
 int kp_solve(kp_ctx *ctx, const kp_params *p, kp_result *stats);

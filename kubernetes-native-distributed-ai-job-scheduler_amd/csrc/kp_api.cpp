@@ -6,13 +6,22 @@
 // one batched solve. Host code here validates, groups the queue
 // into gangs (one LLMService CR = Spec.Replicas identical replicas,
 // llmservice_controller.go:182-203), ranks units, and drives the round/pass
-// loop; every data-parallel step runs in kp_kernels.hip on the GPU. There is
-// no CPU fallback: without a gfx950 device kp_create fails with KP_ENODEV.
+// loop; every data-parallel step runs in the gfx950 kernels of kp_score.hip /
+// kp_pass.hip / kp_preempt.hip. There is no CPU fallback: without a gfx950
+// device kp_create fails with KP_ENODEV.
+//
+// Threading contract (include/kplace.h): every entry point takes the
+// context's mutex for its whole duration (kp_place included: one acquisition
+// for load + solve + fetch) and calls hipSetDevice itself. The detail text of
+// a failure is kept per context (kp_last_error), because cgo callers hop OS
+// threads between calls.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
+#include <cstdarg>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -20,15 +29,43 @@
 #include "kp_internal.hpp"
 
 namespace {
-thread_local std::string g_err;
-}
+thread_local std::string g_err;           // last HIP/RCCL detail on this thread
+thread_local kp_ctx *g_cur = nullptr;     // context of the entry point running here
+}  // namespace
 
 void kp_set_error(const char *what, hipError_t e) {
   g_err = std::string(what) + ": " + hipGetErrorString(e);
+  if (g_cur) g_cur->last_error = g_err;
+}
+
+void kp_set_error_msg(const std::string &msg) {
+  if (g_cur) g_cur->last_error = msg;
 }
 
 namespace kp {
 
+// Entry guard of every public call: the context lock for the whole call, the
+// per-context error slot, and the context's device on this thread.
+struct Entry {
+  kp_ctx *c;
+  std::unique_lock<std::mutex> lk;
+  kp_ctx *prev;
+  explicit Entry(kp_ctx *ctx) : c(ctx), lk(ctx->mu), prev(g_cur) {
+    g_cur = ctx;
+    ctx->last_error.clear();
+  }
+  ~Entry() { g_cur = prev; }
+};
+
+static int fail(int code, const char *fmt, ...) {
+  char buf[256];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  kp_set_error_msg(buf);
+  return code;
+}
 
 static uint32_t fmix32(uint32_t h) {
   h ^= h >> 16;
@@ -41,19 +78,21 @@ static uint32_t fmix32(uint32_t h) {
 
 // ---- validation, identical to oracle/kp_oracle.c check_params/check_nodes ----
 static int check_params(const kp_params *p, int32_t D) {
-  if (!p) return KP_EINVAL;
+  if (!p) return fail(KP_EINVAL, "params: NULL");
   for (int d = 0; d < KP_MAX_DIMS; ++d)
-    if (p->w_dim[d] < 0 || p->w_dim[d] > 65535) return KP_EINVAL;
+    if (p->w_dim[d] < 0 || p->w_dim[d] > 65535) return fail(KP_EINVAL, "params: w_dim[%d]", d);
   if (p->score_mode != KP_SCORE_MOST_ALLOCATED && p->score_mode != KP_SCORE_LEAST_ALLOCATED)
-    return KP_EINVAL;
-  if (p->gpu_dim < -1 || p->gpu_dim >= D) return KP_EINVAL;
-  if (p->w_gpu_fit < 0 || p->w_gpu_fit > (1 << 20)) return KP_EINVAL;
-  if (p->w_spread < 0 || p->w_spread > (1 << 20)) return KP_EINVAL;
-  if (p->tie_mode != KP_TIE_NODE_INDEX && p->tie_mode != KP_TIE_ROTATED) return KP_EINVAL;
-  if (p->max_rounds < 0) return KP_EINVAL;
-  if (p->n_cand < 1 || p->n_cand > KP_MAX_CAND) return KP_EINVAL;
-  if (p->util_scale < 1 || p->util_scale > 1024) return KP_EINVAL;
-  if (p->max_passes < 1 || p->max_passes > 64) return KP_EINVAL;
+    return fail(KP_EINVAL, "params: score_mode");
+  if (p->gpu_dim < -1 || p->gpu_dim >= D) return fail(KP_EINVAL, "params: gpu_dim");
+  if (p->w_gpu_fit < 0 || p->w_gpu_fit > (1 << 20)) return fail(KP_EINVAL, "params: w_gpu_fit");
+  if (p->w_spread < 0 || p->w_spread > (1 << 20)) return fail(KP_EINVAL, "params: w_spread");
+  if (p->tie_mode != KP_TIE_NODE_INDEX && p->tie_mode != KP_TIE_ROTATED)
+    return fail(KP_EINVAL, "params: tie_mode");
+  if (p->max_rounds < 0) return fail(KP_EINVAL, "params: max_rounds");
+  if (p->n_cand < 1 || p->n_cand > KP_MAX_CAND) return fail(KP_EINVAL, "params: n_cand");
+  if (p->util_scale < 1 || p->util_scale > 1024) return fail(KP_EINVAL, "params: util_scale");
+  if (p->max_passes < 1 || p->max_passes > 64) return fail(KP_EINVAL, "params: max_passes");
+  if (p->w_affinity < 0 || p->w_affinity > (1 << 20)) return fail(KP_EINVAL, "params: w_affinity");
   return KP_OK;
 }
 
@@ -66,27 +105,29 @@ static int dalloc(T **p, size_t n) {
   if (n == 0) n = 1;
   if (hipMalloc(reinterpret_cast<void **>(p), n * sizeof(T)) != hipSuccess) {
     *p = nullptr;
-    return KP_ENOMEM;
+    return fail(KP_ENOMEM, "hipMalloc of %zu bytes", n * sizeof(T));
   }
   return KP_OK;
 }
 
-
 static int ensure_nodes(kp_ctx *c, int32_t N, int32_t D) {
   if (N <= c->cap_N && D == c->D && c->d.cap) return KP_OK;
+  c->cap_N = 0;  // a failed (re)allocation leaves no usable node buffers
   const int32_t n = std::max(N, 64);
   KP_TRY(dalloc(&c->d.cap, (size_t)D * n));
   KP_TRY(dalloc(&c->d.used, (size_t)D * n));
   KP_TRY(dalloc(&c->d.used0, (size_t)D * n));
-  KP_TRY(dalloc(&c->d.R, (size_t)D * n));
+  KP_TRY(dalloc(&c->d.R32, (size_t)D * n));
+  KP_TRY(dalloc(&c->d.K32, (size_t)D * n));
   KP_TRY(dalloc(&c->d.base, (size_t)n));
   KP_TRY(dalloc(&c->d.topo, (size_t)n));
   KP_TRY(dalloc(&c->d.seg_start, (size_t)n));
   KP_TRY(dalloc(&c->d.seg_end, (size_t)n));
   KP_TRY(dalloc(&c->d.roff, (size_t)n + 1));
   KP_TRY(dalloc(&c->d.node_flag, (size_t)n));
-  KP_TRY(dalloc(&c->d.node_list, (size_t)n));
-  KP_TRY(dalloc(&c->d.np32, (size_t)(4 * D + 1) * (((size_t)n + 1023) & ~(size_t)1023)));
+  // +4: k_accept's list mode reads node_list[wave] for up to 3 padding waves
+  KP_TRY(dalloc(&c->d.node_list, (size_t)n + 4));
+  KP_TRY(dalloc(&c->d.np32, (size_t)(4 * D + 2) * (((size_t)n + 1023) & ~(size_t)1023)));
   c->cap_N = n;
   return KP_OK;
 }
@@ -94,11 +135,13 @@ static int ensure_nodes(kp_ctx *c, int32_t N, int32_t D) {
 static int ensure_units(kp_ctx *c, int32_t U, int32_t J) {
   const int32_t K = KP_MAX_CAND;
   if (U > c->cap_U) {
+    c->cap_U = 0;
     const size_t u = (size_t)std::max(U, 64);
     KP_TRY(dalloc(&c->d.leader, u));
     KP_TRY(dalloc(&c->d.size, u));
     KP_TRY(dalloc(&c->d.status, u));
     KP_TRY(dalloc(&c->d.salt, u));
+    KP_TRY(dalloc(&c->d.aff, u));
     KP_TRY(dalloc(&c->d.act_local, u));
     KP_TRY(dalloc(&c->d.cand_local, u * K));
     KP_TRY(dalloc(&c->d.open, u));
@@ -140,6 +183,7 @@ static int ensure_units(kp_ctx *c, int32_t U, int32_t J) {
     c->cap_U = (int32_t)u;
   }
   if (J > c->cap_J) {
+    c->cap_J = 0;
     const size_t j = (size_t)std::max(J, 64);
     KP_TRY(dalloc(&c->d.job_node, j));
     KP_TRY(dalloc(&c->d.job_score, j));
@@ -155,17 +199,32 @@ static int ensure_units(kp_ctx *c, int32_t U, int32_t J) {
 static int ensure_q(kp_ctx *c, int32_t U, int32_t D) {
   const int64_t n = (int64_t)D * std::max(U, 64);
   if (n <= c->cap_q && c->d.q) return KP_OK;  // grows only
+  c->cap_q = 0;
   KP_TRY(dalloc(&c->d.q, (size_t)n));
   c->cap_q = n;
   return KP_OK;
 }
 
+// Score matrix of the solve: `rows` rows of stride Ns = round_up(N, 64). Kept
+// across solves and node-table reloads while the stride does not change (a
+// resident ~1 GB buffer at config #3; no hipMalloc/hipFree in the solve).
 static int ensure_matrix(kp_ctx *c, int32_t rows) {
   const int32_t Ns = (c->N + 63) & ~63;
-  if (rows <= c->cap_rows && c->d.score) return KP_OK;
-  KP_TRY(dalloc(&c->d.score, (size_t)rows * Ns));
-  KP_TRY(dalloc(&c->d.mask, (size_t)rows * (Ns / 64)));
+  if (c->d.score && Ns == c->mat_Ns && rows <= c->cap_rows) return KP_OK;
+  c->cap_rows = 0;
+  KP_TRY(dalloc(&c->d.score, (size_t)rows * std::max(Ns, 64)));
   c->cap_rows = rows;
+  c->mat_Ns = Ns;
+  return KP_OK;
+}
+
+// Feasibility bitmask rows of kp_score (never allocated by a solve).
+static int ensure_mask(kp_ctx *c, int32_t rows) {
+  const int32_t words = std::max((c->N + 63) / 64, 1);
+  if (c->d.mask && (int64_t)rows * words <= (int64_t)c->cap_mask_rows) return KP_OK;
+  c->cap_mask_rows = 0;
+  KP_TRY(dalloc(&c->d.mask, (size_t)rows * words));
+  c->cap_mask_rows = (int32_t)std::min<int64_t>((int64_t)rows * words, INT32_MAX);
   return KP_OK;
 }
 
@@ -180,10 +239,13 @@ static ScoreParams make_sp(const kp_ctx *c, const kp_params *p) {
   sp.w_spread = p->w_spread;
   sp.tie_rotated = p->tie_mode == KP_TIE_ROTATED;
   sp.n_cand = p->n_cand;
+  sp.S = p->util_scale;
+  sp.w_affinity = p->w_affinity;
   return sp;
 }
 
-// R table and LeastAllocated base depend on (S, mode, weights): rebuild on change
+// Division tables and LeastAllocated base depend on (S, mode, weights):
+// rebuild on change
 static int prep_for(kp_ctx *c, const kp_params *p) {
   bool same = c->util_scale_loaded == p->util_scale && c->mode_loaded == p->score_mode;
   for (int d = 0; d < KP_MAX_DIMS; ++d) same = same && c->w_loaded[d] == p->w_dim[d];
@@ -203,68 +265,28 @@ static int64_t rows_per_chunk(const kp_ctx *c) {
   return std::min<int64_t>(r, INT32_MAX / std::max<int64_t>(Ns, 64));
 }
 
-struct EvPair {
-  hipEvent_t a = nullptr, b = nullptr;
+// HIP events of one solve, destroyed on every exit path
+struct Events {
+  std::vector<hipEvent_t> ev;
+  ~Events() {
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+  }
+  int make(hipEvent_t *e, unsigned flags) {
+    KP_HIP(hipEventCreateWithFlags(e, flags));
+    ev.push_back(*e);
+    return KP_OK;
+  }
 };
 
-}  // namespace kp
-
-using namespace kp;
-
-extern "C" {
-
-void kp_params_default(kp_params *p) {
-  if (!p) return;
-  static const int32_t w[KP_MAX_DIMS] = {1, 1, 4, 2, 1, 1, 1, 1};
-  std::memset(p, 0, sizeof *p);
-  for (int d = 0; d < KP_MAX_DIMS; ++d) p->w_dim[d] = w[d];
-  p->score_mode = KP_SCORE_MOST_ALLOCATED;
-  p->gpu_dim = 2;
-  p->w_gpu_fit = 1024;
-  p->w_spread = 256;
-  p->tie_mode = KP_TIE_ROTATED;
-  p->tie_seed = 0x6B706C61u;
-  p->max_rounds = 0;
-  p->n_cand = 16;
-  p->util_scale = 100;
-  p->max_passes = 16;
-}
-
-int kp_abi_version(void) { return KP_ABI_VERSION; }
-
-const char *kp_strerror(int code) {
-  switch (code) {
-    case KP_OK: return "ok";
-    case KP_EINVAL: return "invalid argument";
-    case KP_EHIP: return g_err.empty() ? "HIP runtime error" : g_err.c_str();
-    case KP_ERCCL: return g_err.empty() ? "RCCL error" : g_err.c_str();
-    case KP_ENOMEM: return "out of memory";
-    case KP_ESTATE: return "call order violated";
-    case KP_ENODEV: return "no usable gfx950 device";
-  }
-  return "unknown error";
-}
-
-int kp_dist_unique_id(void *out128) {
-  if (!out128) return KP_EINVAL;
-  ncclUniqueId id;
-  if (ncclGetUniqueId(&id) != ncclSuccess) return KP_ERCCL;
-  static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
-  std::memcpy(out128, &id, sizeof id);
-  return KP_OK;
-}
-
-int kp_create(kp_ctx **out, const kp_config *cfg) {
-  if (!out) return KP_EINVAL;
+// ---------------------------------------------------------------------------
+// context creation (one GPU)
+// ---------------------------------------------------------------------------
+int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_id,
+               void *nccl_comm, int64_t max_pairs) {
   *out = nullptr;
-  kp_config def{};
-  def.device = -1;
-  def.world_size = 1;
-  if (!cfg) cfg = &def;
-  if (cfg->world_size < 1 || cfg->rank < 0 || cfg->rank >= cfg->world_size) return KP_EINVAL;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return KP_ENODEV;
-  int dev = cfg->device;
+  int dev = device;
   if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return KP_ENODEV;
   if (dev >= ndev) return KP_ENODEV;
   hipDeviceProp_t prop;
@@ -273,9 +295,9 @@ int kp_create(kp_ctx **out, const kp_config *cfg) {
   kp_ctx *c = new (std::nothrow) kp_ctx();
   if (!c) return KP_ENOMEM;
   c->device = dev;
-  c->world = cfg->world_size;
-  c->rank = cfg->rank;
-  c->max_pairs_matrix = cfg->max_pairs_matrix;
+  c->world = world;
+  c->rank = rank;
+  c->max_pairs_matrix = max_pairs;
   if (const char *e = std::getenv("KP_SELECT_LDS_CAP")) c->select_lds_cap = std::atoi(e);
   if (const char *e = std::getenv("KP_SELECT_GENERIC")) c->select_generic = std::atoi(e) != 0;
   if (const char *e = std::getenv("KP_SELECT_BS")) c->select_bs = std::atoi(e);
@@ -291,11 +313,13 @@ int kp_create(kp_ctx **out, const kp_config *cfg) {
     kp_destroy(c);
     return KP_EHIP;
   }
-  if (c->world > 1 && cfg->nccl_id) {  // else: host-staged exchange (kp_set_allgather)
+  if (nccl_comm) {
+    c->nccl_comm = nccl_comm;
+  } else if (world > 1 && nccl_id) {  // else: host-staged exchange (kp_set_allgather)
     ncclUniqueId id;
-    std::memcpy(&id, cfg->nccl_id, sizeof id);
+    std::memcpy(&id, nccl_id, sizeof id);
     ncclComm_t comm;
-    if (ncclCommInitRank(&comm, c->world, id, c->rank) != ncclSuccess) {
+    if (ncclCommInitRank(&comm, world, id, rank) != ncclSuccess) {
       kp_destroy(c);
       return KP_ERCCL;
     }
@@ -305,69 +329,28 @@ int kp_create(kp_ctx **out, const kp_config *cfg) {
   return KP_OK;
 }
 
-void kp_destroy(kp_ctx *c) {
-  if (!c) return;
-  (void)hipSetDevice(c->device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
-  if (c->nccl_comm) ncclCommDestroy(static_cast<ncclComm_t>(c->nccl_comm));
-  DevState &d = c->d;
-  void *ptrs[] = {d.cap, d.used, d.used0, d.R, d.base, d.topo, d.q, d.leader, d.size, d.status, d.salt,
-                  d.job_node, d.job_score, d.job_status, d.act_local, d.cand_local, d.score,
-                  d.mask, d.open, d.flag, d.s0, d.bid, d.gpart, d.nparts, d.arrive, d.win,
-                  d.inv, d.ent_unit,
-                  d.ent_slot, d.ent_size, d.ent_lead, d.ent_q,
-                  d.csr_kin, d.csr_vin,
-                  d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
-                  d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.roff,
-                  d.rreq, d.rsuf, d.rprio, d.pre_node, d.pre_vict, d.pre_cost,
-                  d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.stats, d.np32};
-  for (void *p : ptrs)
-    if (p) (void)hipFree(p);
-  if (c->world > 1) {
-    if (d.act) (void)hipFree(d.act);
-    if (d.cand) (void)hipFree(d.cand);
-  }
-  if (c->pinned) (void)hipHostFree(c->pinned);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
-  delete c;
-}
-
-int kp_set_allgather(kp_ctx *c, kp_allgather_fn fn, void *user) {
-  if (!c || !fn) return KP_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (c->world < 2 || c->nccl_comm) return KP_ESTATE;  // RCCL contexts exchange on the device
-  c->allgather = fn;
-  c->allgather_user = user;
-  return KP_OK;
-}
-
-int kp_set_profiling(kp_ctx *c, int enable) {
-  if (!c) return KP_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  c->profiling = enable != 0;
-  return KP_OK;
-}
-
-int kp_last_timing(kp_ctx *c, kp_timing *t) {
-  if (!c || !t) return KP_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  *t = c->timing;
-  return KP_OK;
-}
-
 // ---------------------------------------------------------------------------
-int kp_load_nodes(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap, const int64_t *used,
-                  const int32_t *topo) {
-  if (!c) return KP_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (N < 0 || D < 1 || D > KP_MAX_DIMS || (N > 0 && !cap)) return KP_EINVAL;
+// loads (caller holds the lock)
+// ---------------------------------------------------------------------------
+static int load_nodes_impl(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap,
+                           const int64_t *used, const int32_t *topo) {
+  // any failure below leaves no node table (nor the jobs / solve that depend
+  // on it) loaded; sizes are committed only after every copy
+  c->nodes_loaded = false;
+  c->solved = false;
+  if (N < 0 || D < 1 || D > KP_MAX_DIMS || (N > 0 && !cap))
+    return fail(KP_EINVAL, "kp_load_nodes: N=%d D=%d cap=%p", N, D, (const void *)cap);
   for (int64_t i = 0; i < (int64_t)D * N; ++i) {
     const int64_t cc = cap[i], u = used ? used[i] : 0;
-    if (cc < 0 || cc > KP_MAX_VALUE || u < 0 || u > cc) return KP_EINVAL;
+    if (cc < 0 || cc > KP_MAX_VALUE || u < 0 || u > cc)
+      return fail(KP_EINVAL, "kp_load_nodes: dim %lld node %lld: cap %lld used %lld",
+                  (long long)(i / std::max(N, 1)), (long long)(i % std::max(N, 1)),
+                  (long long)cc, (long long)u);
   }
   if (topo)
     for (int32_t n = 0; n < N; ++n)
-      if (topo[n] < 0) return KP_EINVAL;
+      if (topo[n] < 0) return fail(KP_EINVAL, "kp_load_nodes: topo_domain[%d] < 0", n);
+  if (D != c->D) c->jobs_loaded = false;  // request layout depends on D
   KP_HIP(hipSetDevice(c->device));
   try {
     c->h_cap.assign(cap, cap + (size_t)D * N);
@@ -376,15 +359,9 @@ int kp_load_nodes(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap, const int
     c->h_topo.resize(N);
     for (int32_t n = 0; n < N; ++n) c->h_topo[n] = topo ? topo[n] : n;
   } catch (const std::bad_alloc &) {
-    return KP_ENOMEM;
+    return fail(KP_ENOMEM, "kp_load_nodes: host copy");
   }
-  if (D != c->D) c->jobs_loaded = false;  // request layout depends on D
-  c->caps32 = true;
-  for (int64_t i = 0; i < (int64_t)D * N; ++i) c->caps32 = c->caps32 && cap[i] < ((int64_t)1 << 32);
-  c->fits32 = c->caps32 && c->reqs32 && c->jobs_loaded;
   KP_TRY(ensure_nodes(c, N, D));
-  c->N = N;
-  c->D = D;
   if (N > 0) {
     KP_HIP(hipMemcpyAsync(c->d.cap, c->h_cap.data(), sizeof(int64_t) * D * N,
                           hipMemcpyHostToDevice, c->stream));
@@ -396,54 +373,60 @@ int kp_load_nodes(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap, const int
                           hipMemcpyHostToDevice, c->stream));
   }
   // the victim pool belongs to the previous node table
-  c->R = 0;
   KP_HIP(hipMemsetAsync(c->d.roff, 0, sizeof(int32_t) * ((size_t)N + 1), c->stream));
   KP_HIP(hipStreamSynchronize(c->stream));
-  c->util_scale_loaded = 0;  // force an R rebuild at the next solve
-  c->cap_rows = c->d.score ? c->cap_rows : 0;
-  if (c->d.score) {  // row stride depends on N
-    (void)hipFree(c->d.score);
-    (void)hipFree(c->d.mask);
-    c->d.score = nullptr;
-    c->d.mask = nullptr;
-    c->cap_rows = 0;
-  }
+  c->R = 0;
+  c->N = N;
+  c->D = D;
+  c->caps32 = true;
+  for (int64_t i = 0; i < (int64_t)D * N; ++i) c->caps32 = c->caps32 && cap[i] < ((int64_t)1 << 32);
+  c->fits32 = c->caps32 && c->reqs32 && c->jobs_loaded;
+  c->util_scale_loaded = 0;  // force a division-table rebuild at the next solve
   c->nodes_loaded = true;
-  c->solved = false;
   return KP_OK;
 }
 
-int kp_load_jobs(kp_ctx *c, int32_t J, const int64_t *req, const int32_t *prio,
-                 const int32_t *gang_id, const int32_t *gang_size) {
-  if (!c) return KP_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (!c->nodes_loaded) return KP_ESTATE;
+static int load_jobs_impl(kp_ctx *c, int32_t J, const int64_t *req, const int32_t *prio,
+                          const int32_t *gang_id, const int32_t *gang_size,
+                          const int32_t *aff) {
+  c->jobs_loaded = false;  // any failure below leaves no queue loaded
+  c->solved = false;
+  if (!c->nodes_loaded) return fail(KP_ESTATE, "kp_load_jobs: no node table loaded");
   const int32_t D = c->D;
-  if (J < 0 || (J > 0 && !req)) return KP_EINVAL;
+  if (J < 0 || (J > 0 && !req)) return fail(KP_EINVAL, "kp_load_jobs: J=%d req=%p", J, (const void *)req);
   for (int64_t i = 0; i < (int64_t)D * J; ++i)
-    if (req[i] < 0 || req[i] > KP_MAX_VALUE) return KP_EINVAL;
+    if (req[i] < 0 || req[i] > KP_MAX_VALUE)
+      return fail(KP_EINVAL, "kp_load_jobs: req of job %lld dim %lld out of [0, 2^56]",
+                  (long long)(i % std::max(J, 1)), (long long)(i / std::max(J, 1)));
   // units: maximal runs of equal gang_id >= 0 (one CR's replicas); rank order
-  std::vector<int32_t> leader, size, uprio;
+  std::vector<int32_t> leader, size, uprio, uaff;
   try {
     leader.reserve(J);
     size.reserve(J);
     uprio.reserve(J);
+    uaff.reserve(J);
     for (int32_t j = 0; j < J;) {
       const int32_t gid = gang_id ? gang_id[j] : -1;
       int32_t e = j + 1;
       if (gid >= 0)
         while (e < J && gang_id[e] == gid) ++e;
       const int32_t len = e - j;
-      if (len > KP_MAX_GANG) return KP_EINVAL;
+      if (len > KP_MAX_GANG) return fail(KP_EINVAL, "kp_load_jobs: gang %d has %d > 64 members", gid, len);
       for (int32_t k = j; k < e; ++k) {
-        if (gang_size && gang_size[k] != len) return KP_EINVAL;
-        if (prio && prio[k] != prio[j]) return KP_EINVAL;
+        if (gang_size && gang_size[k] != len)
+          return fail(KP_EINVAL, "kp_load_jobs: job %d gang_size %d != run length %d", k, gang_size[k], len);
+        if (prio && prio[k] != prio[j])
+          return fail(KP_EINVAL, "kp_load_jobs: gang %d mixes priorities", gid);
+        if (aff && (aff[k] != aff[j] || aff[k] < -1))
+          return fail(KP_EINVAL, "kp_load_jobs: job %d affinity %d", k, aff[k]);
         for (int d = 0; d < D; ++d)
-          if (req[(int64_t)d * J + k] != req[(int64_t)d * J + j]) return KP_EINVAL;
+          if (req[(int64_t)d * J + k] != req[(int64_t)d * J + j])
+            return fail(KP_EINVAL, "kp_load_jobs: gang %d mixes requests", gid);
       }
       leader.push_back(j);
       size.push_back(len);
       uprio.push_back(prio ? prio[j] : 0);
+      uaff.push_back(aff ? aff[j] : -1);
       j = e;
     }
     if (gang_id) {  // a gang id may not reappear in a later run
@@ -451,7 +434,8 @@ int kp_load_jobs(kp_ctx *c, int32_t J, const int64_t *req, const int32_t *prio,
       for (size_t u = 0; u < leader.size(); ++u)
         if (gang_id[leader[u]] >= 0) ids.push_back(gang_id[leader[u]]);
       std::sort(ids.begin(), ids.end());
-      if (std::adjacent_find(ids.begin(), ids.end()) != ids.end()) return KP_EINVAL;
+      auto it = std::adjacent_find(ids.begin(), ids.end());
+      if (it != ids.end()) return fail(KP_EINVAL, "kp_load_jobs: gang id %d reappears", *it);
     }
     const int32_t U = (int32_t)leader.size();
     std::vector<int32_t> ord(U);
@@ -462,41 +446,45 @@ int kp_load_jobs(kp_ctx *c, int32_t J, const int64_t *req, const int32_t *prio,
     c->h_leader.resize(U);
     c->h_size.resize(U);
     c->h_prio.resize(U);
+    c->h_aff.resize(U);
     c->h_q.resize((size_t)D * U);
     for (int32_t r = 0; r < U; ++r) {
       c->h_leader[r] = leader[ord[r]];
       c->h_size[r] = size[ord[r]];
       c->h_prio[r] = uprio[ord[r]];
+      c->h_aff[r] = uaff[ord[r]];
       for (int d = 0; d < D; ++d)
         c->h_q[(size_t)d * U + r] = req[(int64_t)d * J + leader[ord[r]]];
     }
-    c->J = J;
-    c->U = U;
   } catch (const std::bad_alloc &) {
-    return KP_ENOMEM;
+    return fail(KP_ENOMEM, "kp_load_jobs: host copy");
   }
+  const int32_t U = (int32_t)c->h_leader.size();
   KP_HIP(hipSetDevice(c->device));
-  KP_TRY(ensure_units(c, c->U, J));
-  KP_TRY(ensure_q(c, c->U, D));
-  if (c->U > 0) {
-    KP_HIP(hipMemcpyAsync(c->d.leader, c->h_leader.data(), sizeof(int32_t) * c->U,
+  KP_TRY(ensure_units(c, U, J));
+  KP_TRY(ensure_q(c, U, D));
+  if (U > 0) {
+    KP_HIP(hipMemcpyAsync(c->d.leader, c->h_leader.data(), sizeof(int32_t) * U,
                           hipMemcpyHostToDevice, c->stream));
-    KP_HIP(hipMemcpyAsync(c->d.size, c->h_size.data(), sizeof(int32_t) * c->U,
+    KP_HIP(hipMemcpyAsync(c->d.size, c->h_size.data(), sizeof(int32_t) * U,
                           hipMemcpyHostToDevice, c->stream));
-    KP_HIP(hipMemcpyAsync(c->d.q, c->h_q.data(), sizeof(int64_t) * D * c->U,
+    KP_HIP(hipMemcpyAsync(c->d.q, c->h_q.data(), sizeof(int64_t) * D * U,
                           hipMemcpyHostToDevice, c->stream));
-    KP_HIP(hipMemcpyAsync(c->d.uprio, c->h_prio.data(), sizeof(int32_t) * c->U,
+    KP_HIP(hipMemcpyAsync(c->d.uprio, c->h_prio.data(), sizeof(int32_t) * U,
+                          hipMemcpyHostToDevice, c->stream));
+    KP_HIP(hipMemcpyAsync(c->d.aff, c->h_aff.data(), sizeof(int32_t) * U,
                           hipMemcpyHostToDevice, c->stream));
   }
   KP_HIP(hipStreamSynchronize(c->stream));
+  c->J = J;
+  c->U = U;
   // this rank's shard: a contiguous block of rank positions
-  c->u_lo = (int32_t)((int64_t)c->U * c->rank / c->world);
-  c->u_hi = (int32_t)((int64_t)c->U * (c->rank + 1) / c->world);
+  c->u_lo = (int32_t)((int64_t)U * c->rank / c->world);
+  c->u_hi = (int32_t)((int64_t)U * (c->rank + 1) / c->world);
   c->reqs32 = true;
   for (int64_t i = 0; i < (int64_t)D * J; ++i) c->reqs32 = c->reqs32 && req[i] < ((int64_t)1 << 32);
-  c->jobs_loaded = true;
   c->fits32 = c->caps32 && c->reqs32;
-  c->solved = false;
+  c->jobs_loaded = true;
   return KP_OK;
 }
 
@@ -504,28 +492,29 @@ int kp_load_jobs(kp_ctx *c, int32_t J, const int64_t *req, const int32_t *prio,
 // This rank's candidates -> every rank's, as fixed-size blocks
 // [count, (unit, K candidates) x B] (B: the same slot bound on every rank), so
 // the all-gather needs no host-known count: one collective per round and, over
-// RCCL, no host synchronisation. The host-staged transport (kp_set_allgather)
-// moves the same blocks through host memory.
+// RCCL, no host synchronisation. The host-staged transport (kp_set_allgather,
+// or the in-process exchange of kp_create_multi) moves the same blocks
+// through host memory.
 static int exchange_round(kp_ctx *c, int32_t B, int32_t K) {
   const size_t per = 1 + (size_t)B * (K + 1);
   KP_TRY(launch_pack_exchange(c, B, K));
   if (c->nccl_comm) {
     if (ncclAllGather(c->d.xg_send, c->d.xg_recv, per, ncclInt32,
                       static_cast<ncclComm_t>(c->nccl_comm), c->stream) != ncclSuccess)
-      return KP_ERCCL;
+      return fail(KP_ERCCL, "ncclAllGather of %zu ints", per);
   } else {
     try {
       c->h_xg_send.resize(per);
       c->h_xg_recv.resize(per * c->world);
     } catch (const std::bad_alloc &) {
-      return KP_ENOMEM;
+      return fail(KP_ENOMEM, "exchange staging");
     }
     KP_HIP(hipMemcpyAsync(c->h_xg_send.data(), c->d.xg_send, sizeof(int32_t) * per,
                           hipMemcpyDeviceToHost, c->stream));
     KP_HIP(hipStreamSynchronize(c->stream));
     if (c->allgather(c->allgather_user, c->h_xg_send.data(), sizeof(int32_t) * per,
                      c->h_xg_recv.data()) != 0)
-      return KP_ERCCL;
+      return fail(KP_ERCCL, "host-staged all-gather failed");
     KP_HIP(hipMemcpyAsync(c->d.xg_recv, c->h_xg_recv.data(), sizeof(int32_t) * per * c->world,
                           hipMemcpyHostToDevice, c->stream));
   }
@@ -539,7 +528,11 @@ static double ev_ms(hipEvent_t a, hipEvent_t b) {
 }
 
 static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
+  if (!c->nodes_loaded || !c->jobs_loaded) return fail(KP_ESTATE, "kp_solve: load nodes and jobs first");
+  if (c->world > 1 && !c->nccl_comm && !c->allgather)
+    return fail(KP_ESTATE, "kp_solve: multi-rank context without an exchange");
   KP_TRY(check_params(p, c->D));
+  c->solved = false;
   KP_HIP(hipSetDevice(c->device));
   const ScoreParams sp = make_sp(c, p);
   const int32_t K = p->n_cand, U = c->U, N = c->N;
@@ -559,28 +552,21 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   const int32_t shard = c->u_hi - c->u_lo;
   KP_TRY(ensure_matrix(c, (int32_t)std::min<int64_t>(std::max(shard, 1), rpc)));
 
-  std::vector<EvPair> evs;
+  Events E;  // every event of this solve, destroyed on every exit path
   // timing-only events: no system-scope fence (cache writeback/invalidate)
   // at each record, so the bracket measures the kernel, not the fence
-  auto ev_begin = [&](EvPair &e) -> int {
-    KP_HIP(hipEventCreateWithFlags(&e.a, hipEventDisableSystemFence));
-    KP_HIP(hipEventCreateWithFlags(&e.b, hipEventDisableSystemFence));
-    KP_HIP(hipEventRecord(e.a, c->stream));
-    return KP_OK;
-  };
-  hipEvent_t t0, t1;
-  KP_HIP(hipEventCreate(&t0));
-  KP_HIP(hipEventCreate(&t1));
-  KP_HIP(hipMemsetAsync(c->d.stats, 0, sizeof(SolveStats), c->stream));
-  KP_HIP(hipMemsetAsync(c->d.pass_flag, 0, sizeof(int32_t) * 64, c->stream));
-  KP_HIP(hipEventRecord(t0, c->stream));
   struct KEv {
-    EvPair e;
-    int kind;  // 0 = score, 1 = select
+    hipEvent_t a, b;
     int32_t round;
     int64_t rows_bound;
   };
   std::vector<KEv> kev;
+  hipEvent_t t0, t1;
+  KP_TRY(E.make(&t0, hipEventDefault));
+  KP_TRY(E.make(&t1, hipEventDefault));
+  KP_HIP(hipMemsetAsync(c->d.stats, 0, sizeof(SolveStats), c->stream));
+  KP_HIP(hipMemsetAsync(c->d.pass_flag, 0, sizeof(int32_t) * 64, c->stream));
+  KP_HIP(hipEventRecord(t0, c->stream));
   std::vector<int32_t> round_active;  // exact active units per round (when known)
   kp_timing tm{};
   // filter+score and top-K select of `rows` rows starting at act_local[r0];
@@ -589,16 +575,20 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
                           int32_t round) -> int {
     // profiling brackets the filter+score launch only (each event record is
     // a GPU packet of a few us: the select is timed by rocprofv3 instead)
-    EvPair e1;
-    if (c->profiling) KP_TRY(ev_begin(e1));
+    KEv ke{nullptr, nullptr, round, rows};
+    if (c->profiling) {
+      KP_TRY(E.make(&ke.a, hipEventDisableSystemFence));
+      KP_TRY(E.make(&ke.b, hipEventDisableSystemFence));
+      KP_HIP(hipEventRecord(ke.a, c->stream));
+    }
     // the solve needs only the score matrix: its -1 sentinel is the
     // feasibility filter, so the bit mask (kp_score's second output) is not
     // materialised here
     KP_TRY(launch_score(c, sp, c->d.act_local + r0, rows, c->d.score, nullptr, c->d.q, U,
                         rows_dev));
     if (c->profiling) {
-      KP_HIP(hipEventRecord(e1.b, c->stream));
-      kev.push_back({e1, 0, round, rows});
+      KP_HIP(hipEventRecord(ke.b, c->stream));
+      kev.push_back(ke);
     }
     KP_TRY(launch_select(c, sp, c->d.act_local + r0, rows, c->d.score, c->d.cand_local + r0 * K,
                          rows_dev));
@@ -623,7 +613,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     // still busy with it, so there is no idle gap between rounds. A round
     // that turns out empty is a string of no-op launches and ends the solve.
     hipEvent_t evA;
-    KP_HIP(hipEventCreateWithFlags(&evA, hipEventDisableTiming));
+    KP_TRY(E.make(&evA, hipEventDisableTiming));
     int32_t *A_h = c->pinned + 256;
     int64_t A_bound = shard;
     for (int32_t r = 0; A_bound > 0; ++r) {
@@ -648,7 +638,6 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
       round_active.push_back(*A_h);
       A_bound = *A_h;
     }
-    (void)hipEventDestroy(evA);
   } else {
     // Multi-GPU, device-driven like the single-GPU loop: the local and the
     // global active counts stay on the device (counters[0] / counters[1]);
@@ -656,7 +645,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     // count, which every rank reads asynchronously (the same value on all
     // ranks, so every rank calls the all-gather with the same size).
     hipEvent_t evG;
-    KP_HIP(hipEventCreateWithFlags(&evG, hipEventDisableTiming));
+    KP_TRY(E.make(&evG, hipEventDisableTiming));
     int32_t *Al_h = c->pinned + 256, *G_h = c->pinned + 320;
     int64_t Smax = 0;  // largest shard
     for (int r = 0; r < c->world; ++r)
@@ -690,7 +679,6 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
       round_active.push_back(*Al_h);
       G_bound = *G_h;
     }
-    (void)hipEventDestroy(evG);
   }
   KP_TRY(launch_finalize(c));
   KP_HIP(hipEventRecord(t1, c->stream));
@@ -706,22 +694,15 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   const int64_t pairs = dst.active_sum * N;
   tm.solve_ms = ev_ms(t0, t1);
   for (auto &ke : kev) {
-    const double ms = ev_ms(ke.e.a, ke.e.b);
-    (ke.kind == 0 ? tm.score_ms : tm.select_ms) += ms;
+    tm.score_ms += ev_ms(ke.a, ke.b);
     // algorithmic bytes of the rows the launch actually had (device count)
     int64_t rows = ke.rows_bound;
     if (ke.round < (int32_t)round_active.size())
       rows = std::min<int64_t>(rows, round_active[ke.round]);
-    if (ke.kind == 0)
-      tm.score_bytes += rows * Ns * 4 + (int64_t)8 * c->D * rows +
-                        (int64_t)3 * 8 * c->D * N + 8 * (int64_t)N;
-    else
-      tm.select_bytes += rows * Ns * 4 + rows * K * 4;
-    (void)hipEventDestroy(ke.e.a);
-    (void)hipEventDestroy(ke.e.b);
+    tm.score_bytes += rows * Ns * 4 + (int64_t)8 * c->D * rows + (int64_t)3 * 8 * c->D * N +
+                      8 * (int64_t)N;
+    tm.select_bytes += rows * Ns * 4 + rows * K * 4;
   }
-  (void)hipEventDestroy(t0);
-  (void)hipEventDestroy(t1);
   tm.accept_ms = tm.solve_ms - tm.score_ms - tm.select_ms;
   c->timing = tm;
   int32_t placed = 0;
@@ -745,19 +726,8 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   return KP_OK;
 }
 
-int kp_solve(kp_ctx *c, const kp_params *p, kp_result *stats) {
-  if (!c) return KP_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (!c->nodes_loaded || !c->jobs_loaded) return KP_ESTATE;
-  if (c->world > 1 && !c->nccl_comm && !c->allgather) return KP_ESTATE;  // no exchange
-  try {
-    return solve_impl(c, p, stats);
-  } catch (const std::bad_alloc &) {
-    return KP_ENOMEM;
-  }
-}
-
 static int fetch_impl(kp_ctx *c, kp_result *r) {
+  if (!c->solved) return fail(KP_ESTATE, "kp_fetch: no solve since the last load");
   KP_HIP(hipSetDevice(c->device));
   const int32_t J = c->J;
   if (J > 0) {
@@ -784,42 +754,220 @@ static int fetch_impl(kp_ctx *c, kp_result *r) {
   return KP_OK;
 }
 
+}  // namespace kp
+
+using namespace kp;
+
+extern "C" {
+
+void kp_params_default(kp_params *p) {
+  if (!p) return;
+  static const int32_t w[KP_MAX_DIMS] = {1, 1, 4, 2, 1, 1, 1, 1};
+  std::memset(p, 0, sizeof *p);
+  for (int d = 0; d < KP_MAX_DIMS; ++d) p->w_dim[d] = w[d];
+  p->score_mode = KP_SCORE_MOST_ALLOCATED;
+  p->gpu_dim = 2;
+  p->w_gpu_fit = 1024;
+  p->w_spread = 256;
+  p->tie_mode = KP_TIE_ROTATED;
+  p->tie_seed = 0x6B706C61u;
+  p->max_rounds = 0;
+  p->n_cand = 16;
+  p->util_scale = 100;
+  p->max_passes = 16;
+  p->w_affinity = 512;
+}
+
+int kp_abi_version(void) { return KP_ABI_VERSION; }
+
+const char *kp_strerror(int code) {
+  switch (code) {
+    case KP_OK: return "ok";
+    case KP_EINVAL: return "invalid argument";
+    case KP_EHIP: return "HIP runtime error";
+    case KP_ERCCL: return "RCCL error";
+    case KP_ENOMEM: return "out of memory";
+    case KP_ESTATE: return "call order violated";
+    case KP_ENODEV: return "no usable gfx950 device";
+  }
+  return "unknown error";
+}
+
+const char *kp_last_error(kp_ctx *c) {
+  if (!c) return "";
+  std::lock_guard<std::mutex> g(c->mu);
+  return c->last_error.c_str();
+}
+
+int kp_dist_unique_id(void *out128) {
+  if (!out128) return KP_EINVAL;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return KP_ERCCL;
+  static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
+  std::memcpy(out128, &id, sizeof id);
+  return KP_OK;
+}
+
+int kp_create(kp_ctx **out, const kp_config *cfg) {
+  if (!out) return KP_EINVAL;
+  *out = nullptr;
+  kp_config def{};
+  def.device = -1;
+  def.world_size = 1;
+  if (!cfg) cfg = &def;
+  if (cfg->world_size < 1 || cfg->rank < 0 || cfg->rank >= cfg->world_size) return KP_EINVAL;
+  return create_one(out, cfg->device, cfg->world_size, cfg->rank, cfg->nccl_id, nullptr,
+                    cfg->max_pairs_matrix);
+}
+
+int kp_create_multi(kp_ctx **out, const int32_t *gpu_ids, int32_t n, const kp_config *cfg) {
+  if (!out) return KP_EINVAL;
+  *out = nullptr;
+  if (!gpu_ids || n < 1) return KP_EINVAL;
+  return multi_create(out, gpu_ids, n, cfg ? cfg->max_pairs_matrix : 0);
+}
+
+void kp_destroy(kp_ctx *c) {
+  if (!c) return;
+  if (c->multi) {
+    multi_destroy(c);
+    return;
+  }
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->nccl_comm) ncclCommDestroy(static_cast<ncclComm_t>(c->nccl_comm));
+  DevState &d = c->d;
+  void *ptrs[] = {d.cap, d.used, d.used0, d.R32, d.K32, d.base, d.topo, d.q, d.leader, d.size,
+                  d.status, d.salt, d.aff,
+                  d.job_node, d.job_score, d.job_status, d.act_local, d.cand_local, d.score,
+                  d.mask, d.open, d.flag, d.s0, d.bid, d.gpart, d.nparts, d.arrive, d.win,
+                  d.inv, d.ent_unit,
+                  d.ent_slot, d.ent_size, d.ent_lead, d.ent_q,
+                  d.csr_kin, d.csr_vin,
+                  d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
+                  d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.roff,
+                  d.rreq, d.rsuf, d.rprio, d.pre_node, d.pre_vict, d.pre_cost,
+                  d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.stats, d.np32};
+  for (void *p : ptrs)
+    if (p) (void)hipFree(p);
+  if (c->world > 1) {
+    if (d.act) (void)hipFree(d.act);
+    if (d.cand) (void)hipFree(d.cand);
+  }
+  if (c->pinned) (void)hipHostFree(c->pinned);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int kp_set_allgather(kp_ctx *c, kp_allgather_fn fn, void *user) {
+  if (!c || !fn) return KP_EINVAL;
+  if (c->multi) return KP_ESTATE;  // shards exchange inside the library
+  Entry en(c);
+  if (c->world < 2 || c->nccl_comm) return fail(KP_ESTATE, "kp_set_allgather: not a host-staged multi-rank context");
+  c->allgather = fn;
+  c->allgather_user = user;
+  return KP_OK;
+}
+
+int kp_set_profiling(kp_ctx *c, int enable) {
+  if (!c) return KP_EINVAL;
+  if (c->multi) return multi_run(c, [&](kp_ctx *sh, int) { return kp_set_profiling(sh, enable); }, true);
+  Entry en(c);
+  c->profiling = enable != 0;
+  return KP_OK;
+}
+
+int kp_last_timing(kp_ctx *c, kp_timing *t) {
+  if (!c || !t) return KP_EINVAL;
+  if (c->multi) return multi_run(c, [&](kp_ctx *sh, int) { return kp_last_timing(sh, t); }, false);
+  Entry en(c);
+  *t = c->timing;
+  return KP_OK;
+}
+
+// ---------------------------------------------------------------------------
+int kp_load_nodes(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap, const int64_t *used,
+                  const int32_t *topo) {
+  if (!c) return KP_EINVAL;
+  if (c->multi)
+    return multi_run(c, [&](kp_ctx *sh, int) { return kp_load_nodes(sh, N, D, cap, used, topo); },
+                     true);
+  Entry en(c);
+  return load_nodes_impl(c, N, D, cap, used, topo);
+}
+
+int kp_load_jobs(kp_ctx *c, int32_t J, const int64_t *req, const int32_t *prio,
+                 const int32_t *gang_id, const int32_t *gang_size, const int32_t *aff) {
+  if (!c) return KP_EINVAL;
+  if (c->multi)
+    return multi_run(
+        c, [&](kp_ctx *sh, int) { return kp_load_jobs(sh, J, req, prio, gang_id, gang_size, aff); },
+        true);
+  Entry en(c);
+  return load_jobs_impl(c, J, req, prio, gang_id, gang_size, aff);
+}
+
+int kp_solve(kp_ctx *c, const kp_params *p, kp_result *stats) {
+  if (!c) return KP_EINVAL;
+  if (c->multi)
+    return multi_run(c, [&](kp_ctx *sh, int r) { return kp_solve(sh, p, r == 0 ? stats : nullptr); },
+                     true);
+  Entry en(c);
+  try {
+    return solve_impl(c, p, stats);
+  } catch (const std::bad_alloc &) {
+    return fail(KP_ENOMEM, "kp_solve: host allocation");
+  }
+}
+
 int kp_fetch(kp_ctx *c, kp_result *r) {
   if (!c || !r) return KP_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (!c->solved) return KP_ESTATE;
+  if (c->multi) return multi_run(c, [&](kp_ctx *sh, int) { return kp_fetch(sh, r); }, false);
+  Entry en(c);
   return fetch_impl(c, r);
 }
 
 int kp_place(kp_ctx *c, const kp_snapshot *s, const kp_params *p, kp_result *r) {
   if (!c || !s || !p || !r) return KP_EINVAL;
-  {
-    std::lock_guard<std::mutex> g(c->mu);
-    if (check_params(p, s->D) != KP_OK) return KP_EINVAL;
+  if (c->multi)
+    return multi_run(c,
+                     [&](kp_ctx *sh, int k) {
+                       kp_result none{};  // shard k > 0: same solve, no outputs
+                       return kp_place(sh, s, p, k == 0 ? r : &none);
+                     },
+                     true);
+  Entry en(c);  // one acquisition: load + solve + fetch never interleave
+  KP_TRY(check_params(p, s->D));
+  KP_TRY(load_nodes_impl(c, s->N, s->D, s->cap, s->used, s->topo_domain));
+  KP_TRY(load_jobs_impl(c, s->J, s->req, s->prio, s->gang_id, s->gang_size, s->affinity));
+  try {
+    KP_TRY(solve_impl(c, p, nullptr));
+  } catch (const std::bad_alloc &) {
+    return fail(KP_ENOMEM, "kp_place: host allocation");
   }
-  int rc = kp_load_nodes(c, s->N, s->D, s->cap, s->used, s->topo_domain);
-  if (rc) return rc;
-  rc = kp_load_jobs(c, s->J, s->req, s->prio, s->gang_id, s->gang_size);
-  if (rc) return rc;
-  rc = kp_solve(c, p, nullptr);
-  if (rc) return rc;
-  return kp_fetch(c, r);
+  return fetch_impl(c, r);
 }
 
 int kp_apply_delta(kp_ctx *c, const int32_t *node_idx, const int64_t *delta, int32_t K) {
   if (!c || K < 0 || (K > 0 && (!node_idx || !delta))) return KP_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (!c->nodes_loaded) return KP_ESTATE;
+  if (c->multi)
+    return multi_run(c, [&](kp_ctx *sh, int) { return kp_apply_delta(sh, node_idx, delta, K); },
+                     true);
+  Entry en(c);
+  if (!c->nodes_loaded) return fail(KP_ESTATE, "kp_apply_delta: no node table loaded");
   const int32_t N = c->N, D = c->D;
   for (int32_t k = 0; k < K; ++k)
-    if (node_idx[k] < 0 || node_idx[k] >= N) return KP_EINVAL;
+    if (node_idx[k] < 0 || node_idx[k] >= N)
+      return fail(KP_EINVAL, "kp_apply_delta: node_idx[%d] = %d", k, node_idx[k]);
   for (int64_t i = 0; i < (int64_t)D * K; ++i)
-    if (delta[i] > KP_MAX_VALUE || delta[i] < -KP_MAX_VALUE) return KP_EINVAL;
+    if (delta[i] > KP_MAX_VALUE || delta[i] < -KP_MAX_VALUE)
+      return fail(KP_EINVAL, "kp_apply_delta: |delta| > 2^56");
   if (K == 0) return KP_OK;
   KP_HIP(hipSetDevice(c->device));
   // device-side: atomic apply, check the touched entries against [0, cap],
   // undo on violation (the call is all-or-nothing); one host round trip
   if (K > c->cap_delta) {
+    c->cap_delta = 0;
     KP_TRY(dalloc(&c->d.dl_node, (size_t)K));
     KP_TRY(dalloc(&c->d.dl_delta, (size_t)D * K));
     c->cap_delta = K;
@@ -830,13 +978,15 @@ int kp_apply_delta(kp_ctx *c, const int32_t *node_idx, const int64_t *delta, int
                         c->stream));
   int32_t bad = 0;
   KP_TRY(launch_delta(c, K, &bad));
-  return bad ? KP_EINVAL : KP_OK;
+  if (bad) return fail(KP_EINVAL, "kp_apply_delta: a node would leave [0, cap]; nothing applied");
+  return KP_OK;
 }
 
 int kp_reset_nodes(kp_ctx *c) {
   if (!c) return KP_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (!c->nodes_loaded) return KP_ESTATE;
+  if (c->multi) return multi_run(c, [&](kp_ctx *sh, int) { return kp_reset_nodes(sh); }, true);
+  Entry en(c);
+  if (!c->nodes_loaded) return fail(KP_ESTATE, "kp_reset_nodes: no node table loaded");
   KP_HIP(hipSetDevice(c->device));
   if (c->N > 0)
     KP_HIP(hipMemcpyAsync(c->d.used, c->d.used0, sizeof(int64_t) * c->D * c->N,
@@ -847,10 +997,14 @@ int kp_reset_nodes(kp_ctx *c) {
 int kp_score(kp_ctx *c, const kp_params *p, int32_t job_lo, int32_t job_hi, int32_t *score,
              uint64_t *mask) {
   if (!c) return KP_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (!c->nodes_loaded || !c->jobs_loaded) return KP_ESTATE;
+  if (c->multi)
+    return multi_run(c, [&](kp_ctx *sh, int) { return kp_score(sh, p, job_lo, job_hi, score, mask); },
+                     false);
+  Entry en(c);
+  if (!c->nodes_loaded || !c->jobs_loaded) return fail(KP_ESTATE, "kp_score: load nodes and jobs first");
   KP_TRY(check_params(p, c->D));
-  if (job_lo < 0 || job_hi > c->J || job_lo > job_hi) return KP_EINVAL;
+  if (job_lo < 0 || job_hi > c->J || job_lo > job_hi)
+    return fail(KP_EINVAL, "kp_score: job range [%d, %d) of %d", job_lo, job_hi, c->J);
   KP_HIP(hipSetDevice(c->device));
   const int32_t rows = job_hi - job_lo, N = c->N;
   if (rows == 0 || N == 0) return KP_OK;
@@ -866,7 +1020,9 @@ int kp_score(kp_ctx *c, const kp_params *p, int32_t job_lo, int32_t job_hi, int3
     for (int32_t r = 0; r < rows; ++r) unit_of[r] = u_of_job[job_lo + r];
   }
   const int64_t rpc = std::min<int64_t>(rows_per_chunk(c), std::max(c->cap_U, 1));
-  KP_TRY(ensure_matrix(c, (int32_t)std::min<int64_t>(rows, rpc)));
+  const int32_t chunk = (int32_t)std::min<int64_t>(rows, rpc);
+  KP_TRY(ensure_matrix(c, chunk));
+  KP_TRY(ensure_mask(c, chunk));
   std::vector<int32_t> hs;
   std::vector<uint64_t> hm;
   KP_TRY(launch_pack(c));  // 32-bit node planes of the current usage
@@ -893,9 +1049,13 @@ int kp_score(kp_ctx *c, const kp_params *p, int32_t job_lo, int32_t job_hi, int3
 int kp_load_running(kp_ctx *c, int32_t R, const int32_t *node, const int64_t *req,
                     const int32_t *prio) {
   if (!c) return KP_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (!c->nodes_loaded) return KP_ESTATE;
-  if (R < 0 || (R > 0 && (!node || !req || !prio))) return KP_EINVAL;
+  if (c->multi)  // preemption runs on shard 0 only (kp_preempt)
+    return multi_run(c, [&](kp_ctx *sh, int) { return kp_load_running(sh, R, node, req, prio); },
+                     false);
+  Entry en(c);
+  if (!c->nodes_loaded) return fail(KP_ESTATE, "kp_load_running: no node table loaded");
+  if (R < 0 || (R > 0 && (!node || !req || !prio)))
+    return fail(KP_EINVAL, "kp_load_running: R=%d", R);
   const int32_t N = c->N, D = c->D;
   std::vector<int32_t> ord, off;
   std::vector<int64_t> sum, rreq, rsuf, cur;
@@ -904,7 +1064,7 @@ int kp_load_running(kp_ctx *c, int32_t R, const int32_t *node, const int64_t *re
   try {
     cur.resize((size_t)D * N + 1);
   } catch (const std::bad_alloc &) {
-    return KP_ENOMEM;
+    return fail(KP_ENOMEM, "kp_load_running: host copy");
   }
   if (N > 0)
     KP_HIP(hipMemcpyAsync(cur.data(), c->d.used, sizeof(int64_t) * D * N, hipMemcpyDeviceToHost,
@@ -916,11 +1076,12 @@ int kp_load_running(kp_ctx *c, int32_t R, const int32_t *node, const int64_t *re
     sum.assign((size_t)D * N + 1, 0);
     for (int32_t r = 0; r < R; ++r) {
       const int32_t n = node[r];
-      if (n < 0 || n >= N) return KP_EINVAL;
+      if (n < 0 || n >= N) return fail(KP_EINVAL, "kp_load_running: node[%d] = %d", r, n);
       for (int d = 0; d < D; ++d) {
         const int64_t q = req[(int64_t)d * R + r];
-        if (q < 0 || q > KP_MAX_VALUE) return KP_EINVAL;
-        if ((sum[(size_t)d * N + n] += q) > cur[(size_t)d * N + n]) return KP_EINVAL;
+        if (q < 0 || q > KP_MAX_VALUE) return fail(KP_EINVAL, "kp_load_running: req of %d", r);
+        if ((sum[(size_t)d * N + n] += q) > cur[(size_t)d * N + n])
+          return fail(KP_EINVAL, "kp_load_running: running jobs on node %d exceed its usage", n);
       }
     }
     // node-major CSR in reprieve order: (node, prio desc, running index asc)
@@ -951,10 +1112,11 @@ int kp_load_running(kp_ctx *c, int32_t R, const int32_t *node, const int64_t *re
         }
       }
   } catch (const std::bad_alloc &) {
-    return KP_ENOMEM;
+    return fail(KP_ENOMEM, "kp_load_running: host arrays");
   }
-  KP_HIP(hipSetDevice(c->device));
+  c->R = 0;  // no pool until every copy succeeded
   if (R > c->cap_R) {
+    c->cap_R = 0;
     KP_TRY(dalloc(&c->d.rreq, (size_t)D * R));
     KP_TRY(dalloc(&c->d.rsuf, (size_t)D * R));
     KP_TRY(dalloc(&c->d.rprio, (size_t)R));
@@ -977,8 +1139,9 @@ int kp_load_running(kp_ctx *c, int32_t R, const int32_t *node, const int64_t *re
 
 int kp_preempt(kp_ctx *c, kp_preemption *out) {
   if (!c || !out) return KP_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (!c->solved) return KP_ESTATE;
+  if (c->multi) return multi_run(c, [&](kp_ctx *sh, int) { return kp_preempt(sh, out); }, false);
+  Entry en(c);
+  if (!c->solved) return fail(KP_ESTATE, "kp_preempt: no solve since the last load");
   KP_HIP(hipSetDevice(c->device));
   int32_t P = 0;
   KP_TRY(launch_preempt(c, &P));

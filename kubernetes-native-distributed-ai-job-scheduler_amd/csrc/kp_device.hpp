@@ -116,28 +116,109 @@ __device__ __forceinline__ int64_t group_max_i64(int64_t v) {
   return readlane_i64(v, 63);
 }
 
-// §2.3: score of one more copy of q on a node whose usage is `used`;
-// -1 when it does not fit. 64-bit exact; util = ((used+q) * R) >> 32 with
-// R = floor(S * 2^32 / cap) never overflows because used + q <= cap.
+// ---------------------------------------------------------------------------
+// §2.3 exact utilisation, kube-scheduler's integer formulas per dimension:
+//   MostAllocated  util = floor(x*S/c)        (mostRequestedScore)
+//   LeastAllocated util = floor((c-x)*S/c)    (leastRequestedScore)
+//                       = S - ceil(x*S/c)
+// for x = used + q <= c, c > 0 (cap-0 dims contribute 0).
+//
+// 32-bit form (every cap < 2^32): per node and dim a multiplier R and shift
+// k (div_prep) make t = (x*R) >> k equal floor(x*S/c) or one less for every
+// x <= c (x < 2^k and R = floor(S*2^k/c): x*R/2^k lies in (v - 1, v]); one
+// remainder check r = x*S - t*c >= c repairs it. Modes, chosen per node:
+//   E (c < 2^12): R = floor(S*2^k/c) + 1 with c^2 < 2^k: t is exact, no
+//     check (x*R/2^k = v + x*d/2^k with x*d/2^k < 1/c);
+//   C (c < 2^24, S*2^k < 2^32): every product fits 32 bits and every
+//     operand 24 bits: full-rate v_mul_u32_u24 throughout;
+//   W (otherwise): k = 32, 64-bit products (quarter rate, rare).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kDivE = 0x100u, kDivW = 0x200u;  // K plane: shift | mode bits
+
+__host__ __device__ inline void div_prep(uint64_t c, uint32_t S, uint32_t &R, uint32_t &K) {
+  if (c == 0) {  // feasible x = 0: t = 0
+    R = 0;
+    K = 1u | kDivE;
+    return;
+  }
+  int fl = 63;
+  while (!((c >> fl) & 1ull)) --fl;  // floor(log2 c)
+  if (c < (1u << 12)) {
+    const int kE = 2 * fl + 2;  // c^2 < 2^kE
+    const uint64_t top = (uint64_t)S << kE;
+    const uint64_t RE = top / c + 1;
+    if (top + c < (1ull << 32) && RE < (1u << 24)) {
+      R = (uint32_t)RE;
+      K = (uint32_t)kE | kDivE;
+      return;
+    }
+  }
+  const int kC = fl + 1;
+  if (c < (1u << 24) && ((uint64_t)S << kC) < (1ull << 32)) {
+    R = (uint32_t)(((uint64_t)S << kC) / c);
+    K = (uint32_t)kC;
+    return;
+  }
+  R = (uint32_t)(((uint64_t)S << 32) / c);  // c >= 2^21 here: R < 2^32
+  K = 32u | kDivW;
+}
+
+// generic 32-bit form (any mode): floor(x*S/c) for x <= c < 2^32, plus
+// whether the remainder is non-zero (LeastAllocated's ceiling)
+__device__ __forceinline__ uint32_t div_floor32(uint32_t x, uint32_t c, uint32_t R, uint32_t K,
+                                                uint32_t S, bool &rem_nz) {
+  uint32_t t = (uint32_t)(((uint64_t)x * R) >> (K & 63u));
+  uint64_t r = (uint64_t)x * S - (uint64_t)t * c;
+  const uint64_t cc = c ? c : 1;
+  if (r >= cc) {
+    ++t;
+    r -= cc;
+  }
+  rem_nz = r != 0;
+  return t;
+}
+
+// 64-bit form (some cap >= 2^32, caps <= 2^56): x*S needs up to 67 bits. A
+// double estimate (|error| << 1) corrected with 128-bit remainders.
+__device__ __forceinline__ int64_t util64(int64_t x, int64_t c, int32_t S, bool most) {
+  if (x > c) x = c;  // infeasible pair: any value (masked by the caller)
+  const uint64_t y = most ? (uint64_t)x : (uint64_t)(c - x);
+  const unsigned __int128 n = (unsigned __int128)y * (uint32_t)S;
+  uint64_t t = (uint64_t)((double)y * (double)S / (double)c);
+  __int128 r = (__int128)n - (__int128)((unsigned __int128)t * (uint64_t)c);
+  for (int i = 0; i < 4 && r < 0; ++i) {
+    --t;
+    r += c;
+  }
+  for (int i = 0; i < 4 && r >= (__int128)c; ++i) {
+    ++t;
+    r -= c;
+  }
+  return (int64_t)t;
+}
+
+// §2.3: score of one more copy of q on a node whose usage is `used`, in the
+// topo domain `topo`, for a unit preferring domain `aff`; -1 when it does not
+// fit. 64-bit exact (the int64 path).
 template <int D>
 __device__ __forceinline__ int64_t score_at(const ScoreParams &sp, const int64_t (&q)[D],
                                             const int64_t (&cap)[D], const int64_t (&used)[D],
-                                            const uint64_t (&R)[D], int64_t base) {
+                                            int32_t topo, int32_t aff) {
   int64_t acc = 0;
   bool fits = true;
 #pragma unroll
   for (int d = 0; d < D; ++d) {
     fits &= q[d] <= cap[d] - used[d];
-    uint64_t u = (uint64_t)(used[d] + q[d]);
-    uint64_t util = (u * R[d]) >> 32;
-    acc += (int64_t)sp.w[d] * (int64_t)util;
+    if (cap[d] > 0)
+      acc += (int64_t)sp.w[d] * util64(used[d] + q[d], cap[d], sp.S, sp.most_allocated != 0);
   }
-  int64_t s = sp.most_allocated ? acc : base - acc;
+  int64_t s = acc;
   if (sp.gpu_dim >= 0) {
 #pragma unroll
     for (int d = 0; d < D; ++d)
       if (d == sp.gpu_dim && q[d] > 0 && cap[d] - used[d] - q[d] == 0) s += sp.w_gpu_fit;
   }
+  if (aff >= 0 && topo == aff) s += sp.w_affinity;
   return fits ? s : -1;
 }
 

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -44,19 +45,22 @@ struct ScoreParams {
   int32_t w_spread;
   int32_t tie_rotated;
   int32_t n_cand;
+  int32_t S;           // util_scale
+  int32_t w_affinity;  // CacheStrategy "shared" bonus
 };
 
 // Device buffers of one context. Node table SoA [D][N]; units in rank order.
 struct DevState {
   // node table (resident across solves; `used` is committed into)
   int64_t *cap = nullptr, *used = nullptr, *used0 = nullptr;  // used0: as loaded
-  uint64_t *R = nullptr;  // floor(S*2^32/cap), 0 if cap == 0
-  int64_t *base = nullptr;
+  uint32_t *R32 = nullptr, *K32 = nullptr;  // [D][N] exact-division tables (div_prep)
+  int64_t *base = nullptr;  // LeastAllocated base: sum of w*S over dims with cap > 0
   int32_t *topo = nullptr;
-  uint32_t *np32 = nullptr;  // [4*D+1][round_up(N,1024)] 32-bit score tile planes (k_pack32)
+  uint32_t *np32 = nullptr;  // [4*D+2][round_up(N,1024)] 32-bit score tile planes
   // units (rank order), job outputs
   int64_t *q = nullptr;  // [D][U]
   int32_t *leader = nullptr, *size = nullptr, *status = nullptr;
+  int32_t *aff = nullptr;  // [U] affinity topo domain, -1 = none
   uint32_t *salt = nullptr;
   int32_t *job_node = nullptr, *job_score = nullptr, *job_status = nullptr;
   // round scratch
@@ -113,8 +117,13 @@ struct DevState {
 
 }  // namespace kp
 
+namespace kp {
+struct Multi;  // kp_multi.cpp: one context over several GPUs (kp_create_multi)
+}
+
 struct kp_ctx {
   std::mutex mu;
+  kp::Multi *multi = nullptr;  // non-null: this context forwards to its shards
   int device = 0;
   int world = 1, rank = 0;
   void *nccl_comm = nullptr;  // ncclComm_t
@@ -140,6 +149,8 @@ struct kp_ctx {
   // sizes
   int32_t N = 0, D = 0, J = 0, U = 0, R = 0, cap_R = 0, cap_delta = 0;
   int32_t cap_N = 0, cap_U = 0, cap_J = 0, cap_rows = 0, cap_props = 0, cap_K = 0;
+  int32_t mat_Ns = 0;          // row stride the score matrix was allocated for
+  int32_t cap_mask_rows = 0;   // rows of d.mask (kp_score only)
   int64_t cap_q = 0;           // int64 entries of d.q
   int32_t u_lo = 0, u_hi = 0;  // this rank's shard of units (rank positions)
   bool nodes_loaded = false, jobs_loaded = false, solved = false;
@@ -151,14 +162,14 @@ struct kp_ctx {
   // host mirrors
   std::vector<int64_t> h_cap, h_used;
   std::vector<int32_t> h_topo;
-  std::vector<int32_t> h_leader, h_size, h_prio;
+  std::vector<int32_t> h_leader, h_size, h_prio, h_aff;
   std::vector<int64_t> h_q;
   // pinned host scratch
   int32_t *pinned = nullptr;  // small counters
   kp::DevState d;
   kp_result last{};
   kp_timing timing{};
-  std::string last_error;
+  std::string last_error;  // detail of the last failed call (kp_last_error)
 };
 
 // Kernel launchers (kp_score.hip, kp_pass.hip).
@@ -193,6 +204,18 @@ int launch_unpack_exchange(kp_ctx *c, int32_t world, int32_t B, int32_t K);
 size_t rocprim_temp_bytes(int32_t max_items);
 int launch_preempt(kp_ctx *c, int32_t *P_host);
 int launch_delta(kp_ctx *c, int32_t K, int32_t *bad_host);
+
+// context over one GPU (kp_api.cpp); nccl_comm, if given, is adopted
+int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_id,
+               void *nccl_comm, int64_t max_pairs);
+// kp_create_multi (kp_multi.cpp): one context over n GPUs, one worker thread
+// per GPU, each with its own single-GPU shard context
+int multi_create(kp_ctx **out, const int32_t *gpu_ids, int32_t n, int64_t max_pairs);
+void multi_destroy(kp_ctx *c);
+// Runs fn(shard, index) on every shard's worker thread (all) or on shard 0
+// only, under the multi context's lock; returns the first failure (by shard
+// index) and copies that shard's kp_last_error text.
+int multi_run(kp_ctx *c, const std::function<int(kp_ctx *, int)> &fn, bool all);
 }  // namespace kp
 
 #define KP_HIP(expr)                                                \
@@ -205,6 +228,8 @@ int launch_delta(kp_ctx *c, int32_t K, int32_t *bad_host);
   } while (0)
 
 void kp_set_error(const char *what, hipError_t e);
+// detail text for a non-HIP failure of the current call (kp_last_error)
+void kp_set_error_msg(const std::string &msg);
 
 #define KP_TRY(expr)              \
   do {                            \

@@ -124,11 +124,11 @@ struct PlanArgs {
   uint8_t *open;
   int32_t *status;
   const int64_t *cap, *used;
-  const uint64_t *R;
+  const uint32_t *R32, *K32;
   const int64_t *base;
   const int32_t *topo;
   const int64_t *q;
-  const int32_t *size;
+  const int32_t *size, *aff;
   uint32_t *bid;
   int32_t *win, *s0_out, *pass_flag;
   int4 *gpart;
@@ -159,6 +159,7 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
   if (__ballot(slot_ok) == 0) return;
   const int32_t u = slot_ok ? u0 : 0;
   const int32_t sz = slot_ok ? pa.size[u] : 0;
+  const int32_t af = slot_ok ? pa.aff[u] : -1;
   int64_t qq[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) qq[d] = slot_ok ? pa.q[(int64_t)d * U + u] : 0;
@@ -173,31 +174,32 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
   if constexpr (W32) {
     // every cap and request < 2^32 (fits32): the remaining free capacity and
     // the usage after the planned members are tracked incrementally, so no
-    // product of a member count overflows; util = mulhi(x, Rl) + x*Rh is
-    // exact (k_score32) and every score fits an int32
-    uint32_t q32[D], rem[D], uu[D], rl[D], rh[D];
+    // product of a member count overflows; the exact division of div_prep
+    // (kp_device.hpp, generic form) and every score fit 32 bits
+    uint32_t q32[D], rem[D], uu[D], cc[D], rr[D], kk[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       q32[d] = (uint32_t)qq[d];
-      const uint64_t rr = pa.R[(int64_t)d * N + nn];
       uu[d] = (uint32_t)pa.used[(int64_t)d * N + nn];
-      rem[d] = (uint32_t)pa.cap[(int64_t)d * N + nn] - uu[d];
-      rl[d] = (uint32_t)rr;
-      rh[d] = (uint32_t)(rr >> 32);
+      cc[d] = (uint32_t)pa.cap[(int64_t)d * N + nn];
+      rem[d] = cc[d] - uu[d];
+      rr[d] = pa.R32[(int64_t)d * N + nn];
+      kk[d] = pa.K32[(int64_t)d * N + nn];
     }
     const int32_t b = (int32_t)pa.base[nn];
     const int g = sp.gpu_dim;
+    const int32_t abonus = (af >= 0 && tp == af) ? sp.w_affinity : 0;
     for (int m = 0; m < szmax; ++m) {
       const bool live = !fail && m < sz;  // group-uniform
       bool fits = live && valid;
-      int32_t acc = 0, bonus = 0;
+      int32_t acc = 0, bonus = abonus;
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         fits &= q32[d] <= rem[d];
-        const uint32_t x = uu[d] + q32[d];
-        const uint32_t util = __umulhi(x, rl[d]) + x * rh[d];
-        acc += sp.w[d] * (int32_t)util;
-        if (d == g && q32[d] > 0 && rem[d] == q32[d]) bonus = sp.w_gpu_fit;
+        bool nz;
+        const uint32_t t = div_floor32(uu[d] + q32[d], cc[d], rr[d], kk[d], (uint32_t)sp.S, nz);
+        acc += sp.w[d] * (int32_t)(sp.most_allocated ? t : t + (nz ? 1u : 0u));
+        if (d == g && q32[d] > 0 && rem[d] == q32[d]) bonus += sp.w_gpu_fit;
       }
       const int32_t s = fits ? (sp.most_allocated ? acc : b - acc) + bonus : -1;
       if (m == 0) s0 = s;
@@ -223,20 +225,17 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
     }
   } else {
     int64_t c_[D], u0_[D];
-    uint64_t r_[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       c_[d] = pa.cap[(int64_t)d * N + nn];
       u0_[d] = pa.used[(int64_t)d * N + nn];
-      r_[d] = pa.R[(int64_t)d * N + nn];
     }
-    const int64_t b = pa.base[nn];
     for (int m = 0; m < szmax; ++m) {
       const bool live = !fail && m < sz;  // group-uniform
       int64_t uu[D];
 #pragma unroll
       for (int d = 0; d < D; ++d) uu[d] = u0_[d] + (int64_t)planned * qq[d];
-      const int64_t s = (live && valid) ? score_at<D>(sp, qq, c_, uu, r_, b) : -1;
+      const int64_t s = (live && valid) ? score_at<D>(sp, qq, c_, uu, tp, af) : -1;
       if (m == 0) s0 = (int32_t)s;
       const bool feas = s >= 0;
       const int64_t val = feas ? s - (int64_t)sp.w_spread * dom : INT64_MIN;
@@ -517,7 +516,9 @@ static PlanArgs plan_args(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t p
   pa.status = c->d.status;
   pa.cap = c->d.cap;
   pa.used = c->d.used;
-  pa.R = c->d.R;
+  pa.R32 = c->d.R32;
+  pa.K32 = c->d.K32;
+  pa.aff = c->d.aff;
   pa.base = c->d.base;
   pa.topo = c->d.topo;
   pa.q = c->d.q;

@@ -21,17 +21,20 @@ namespace {
 using namespace dev;
 
 // ---------------------------------------------------------------------------
-// node prep: R = floor(S*2^32/cap), LeastAllocated base
+// node prep: exact-division tables (div_prep) and the LeastAllocated base
 // ---------------------------------------------------------------------------
-__global__ void k_prep_nodes(const int64_t *__restrict__ cap, uint64_t *__restrict__ R,
-                             int64_t *__restrict__ base, int32_t N, int32_t D, int32_t S,
-                             int32_t least, ScoreParams sp) {
+__global__ void k_prep_nodes(const int64_t *__restrict__ cap, uint32_t *__restrict__ R32,
+                             uint32_t *__restrict__ K32, int64_t *__restrict__ base, int32_t N,
+                             int32_t D, int32_t S, int32_t least, ScoreParams sp) {
   int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
   int64_t b = 0;
   for (int d = 0; d < D; ++d) {
-    int64_t c = cap[(int64_t)d * N + n];
-    R[(int64_t)d * N + n] = c > 0 ? (((uint64_t)S) << 32) / (uint64_t)c : 0;
+    const int64_t c = cap[(int64_t)d * N + n];
+    uint32_t r = 0, k = 0;
+    if (c < ((int64_t)1 << 32)) div_prep((uint64_t)c, (uint32_t)S, r, k);
+    R32[(int64_t)d * N + n] = r;
+    K32[(int64_t)d * N + n] = k;
     if (c > 0) b += (int64_t)sp.w[d] * S;
   }
   base[n] = least ? b : 0;
@@ -63,9 +66,9 @@ template <int D, int NPL>
 __global__ __launch_bounds__(256) void k_score(ScoreParams sp,
                                                const int64_t *__restrict__ cap,
                                                const int64_t *__restrict__ used,
-                                               const uint64_t *__restrict__ R,
-                                               const int64_t *__restrict__ base,
+                                               const int32_t *__restrict__ topo,
                                                const int64_t *__restrict__ q, int32_t qstride,
+                                               const int32_t *__restrict__ uaff,
                                                const int32_t *__restrict__ rows_unit,
                                                int32_t rows, int32_t rows_per_block,
                                                int32_t min_rpb, int32_t *__restrict__ score,
@@ -76,8 +79,8 @@ __global__ __launch_bounds__(256) void k_score(ScoreParams sp,
   const int N = sp.N;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int tile0 = blockIdx.x * (256 * NPL) + wave * (64 * NPL);
-  int64_t c_[NPL][D], u_[NPL][D], b_[NPL];
-  uint64_t r_[NPL][D];
+  int64_t c_[NPL][D], u_[NPL][D];
+  int32_t t_[NPL];
   bool v_[NPL];
 #pragma unroll
   for (int k = 0; k < NPL; ++k) {
@@ -88,9 +91,8 @@ __global__ __launch_bounds__(256) void k_score(ScoreParams sp,
     for (int d = 0; d < D; ++d) {
       c_[k][d] = cap[(int64_t)d * N + nn];
       u_[k][d] = used[(int64_t)d * N + nn];
-      r_[k][d] = R[(int64_t)d * N + nn];
     }
-    b_[k] = base[nn];
+    t_[k] = topo[nn];
   }
   const int words = Ns >> 6;
   const int r0 = blockIdx.y * rows_per_block;
@@ -101,11 +103,12 @@ __global__ __launch_bounds__(256) void k_score(ScoreParams sp,
     int64_t qq[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) qq[d] = q[(int64_t)d * qstride + unit];
+    const int32_t af = uaff[unit];
     int32_t *srow = score + (int64_t)r * Ns;
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
       const int n = tile0 + k * 64 + lane;
-      int64_t s = score_at<D>(sp, qq, c_[k], u_[k], r_[k], b_[k]);
+      int64_t s = score_at<D>(sp, qq, c_[k], u_[k], t_[k], af);
       if (!v_[k]) s = -1;
       const bool feas = s >= 0;
       if (score && n < Ns) srow[n] = feas ? (int32_t)s : KP_SCORE_INFEASIBLE;
@@ -117,12 +120,11 @@ __global__ __launch_bounds__(256) void k_score(ScoreParams sp,
 }
 
 // 32-bit specialisation, chosen by the host when every cap and req is < 2^32
-// (then used+q <= cap < 2^32 on every feasible pair). Same result bit for bit:
-// util = ((u * R) >> 32) with R = Rh*2^32 + Rl (Rh <= S) is
-// mulhi(u, Rl) + u*Rh exactly, since u*Rh*2^32 is a multiple of 2^32.
-// Halves the VALU work per pair so the kernel stays on the HBM store roof.
+// (then used+q <= cap < 2^32 on every feasible pair). Same result bit for bit
+// as the 64-bit path: the exact division of div_prep (kp_device.hpp), whose
+// C and E modes run on full-rate 24-bit multiplies only.
 //
-// Layout: lane l of wave w owns the 4 CONSECUTIVE nodes tile0 + 4l .. +3, so a
+// Layout: lane l of wave w owns the NPL CONSECUTIVE nodes tile0 + NPL*l .., so a
 // row's scores leave as one 16-B store per lane (1 KiB per wave instruction,
 // whole 128-B lines). The 4 per-k ballots are bit-interleaved into the row's
 // 4 mask words (word i bit 4j+k = ballot_k bit 16i+j). The requests of the
@@ -148,36 +150,33 @@ __device__ __forceinline__ uint32_t mul_u24(uint32_t a, uint32_t b) {
   return r;
 }
 
-// bits [47:32] of the 48-bit product of two 24-bit operands (full rate)
-__device__ __forceinline__ uint32_t mulhi_u24(uint32_t a, uint32_t b) {
-  uint32_t r;
-  asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
 
 // Round-start pack of the node table into the 32-bit form k_score32 consumes:
-// u32 SoA planes [4*d + {0: free, 1: used, 2: R lo, 3: R hi}][P] and the
-// LeastAllocated base in plane 4*D, P = round_up(N, 1024) (whole score tiles;
-// padding nodes are zero and masked in the kernel). One 16-B load per lane
-// and plane then fetches a lane's 4 consecutive nodes: 4*D+1 fully coalesced
-// loads per wave instead of 3*D*4 strided 8-B gathers from the int64 table.
+// u32 SoA planes [4*d + {0: free, 1: used, 2: R, 3: K}][P] (div_prep tables),
+// the LeastAllocated base in plane 4*D and the topo domain in plane 4*D+1,
+// P = round_up(N, 1024) (whole score tiles; padding nodes are zero and masked
+// in the kernel). One 8- or 16-B load per lane and plane then fetches a
+// lane's consecutive nodes: 4*D+2 fully coalesced loads per wave instead of
+// strided gathers from the int64 table.
 template <int D>
 __device__ __forceinline__ void pack_node(const int64_t *__restrict__ cap,
                                           const int64_t *__restrict__ used,
-                                          const uint64_t *__restrict__ R,
-                                          const int64_t *__restrict__ base, int32_t N, int32_t P,
+                                          const uint32_t *__restrict__ R32,
+                                          const uint32_t *__restrict__ K32,
+                                          const int64_t *__restrict__ base,
+                                          const int32_t *__restrict__ topo, int32_t N, int32_t P,
                                           uint32_t *__restrict__ np, int n) {
   const bool v = n < N;
 #pragma unroll
   for (int d = 0; d < D; ++d) {
     const int64_t cc = v ? cap[(int64_t)d * N + n] : 0, uu = v ? used[(int64_t)d * N + n] : 0;
-    const uint64_t rr = v ? R[(int64_t)d * N + n] : 0;
     np[(int64_t)(4 * d + 0) * P + n] = (uint32_t)(cc - uu);
     np[(int64_t)(4 * d + 1) * P + n] = (uint32_t)uu;
-    np[(int64_t)(4 * d + 2) * P + n] = (uint32_t)rr;
-    np[(int64_t)(4 * d + 3) * P + n] = (uint32_t)(rr >> 32);
+    np[(int64_t)(4 * d + 2) * P + n] = v ? R32[(int64_t)d * N + n] : 0u;
+    np[(int64_t)(4 * d + 3) * P + n] = v ? K32[(int64_t)d * N + n] : (1u | kDivE);
   }
   np[(int64_t)(4 * D) * P + n] = v ? (uint32_t)base[n] : 0u;
+  np[(int64_t)(4 * D + 1) * P + n] = v ? (uint32_t)topo[n] : 0xFFFFFFFFu;
 }
 
 // Round start, one launch: active-unit flags of [lo, hi) (input of the
@@ -189,12 +188,14 @@ __global__ __launch_bounds__(256) void k_round_start(const int32_t *__restrict__
                                                      int32_t *__restrict__ flag,
                                                      const int64_t *__restrict__ cap,
                                                      const int64_t *__restrict__ used,
-                                                     const uint64_t *__restrict__ R,
-                                                     const int64_t *__restrict__ base, int32_t N,
+                                                     const uint32_t *__restrict__ R32,
+                                                     const uint32_t *__restrict__ K32,
+                                                     const int64_t *__restrict__ base,
+                                                     const int32_t *__restrict__ topo, int32_t N,
                                                      int32_t P, uint32_t *__restrict__ np) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < hi - lo) flag[i] = status[lo + i] == kActive ? 1 : 0;
-  if (i < P) pack_node<D>(cap, used, R, base, N, P, np, i);
+  if (i < P) pack_node<D>(cap, used, R32, K32, base, topo, N, P, np, i);
 }
 
 // bit j of a 32-bit value -> bit 2j
@@ -227,6 +228,7 @@ template <int D, bool MOST, int NPL>
 __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
                                                  const uint32_t *__restrict__ np, int32_t P,
                                                  const int64_t *__restrict__ q, int32_t qstride,
+                                                 const int32_t *__restrict__ uaff,
                                                  const int32_t *__restrict__ rows_unit,
                                                  int32_t rows, int32_t rows_per_block,
                                                  int32_t min_rpb, int32_t *__restrict__ score,
@@ -236,7 +238,9 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
   using V = Vec<NPL>;
   if (rows_dev) fit_rows(*rows_dev, min_rpb, rows, rows_per_block);
   if ((int)blockIdx.y * rows_per_block >= rows) return;  // block-uniform
-  __shared__ uint32_t sq[kScoreMaxRows][D + 1];  // [D] = request in the GPU dim (0 if none)
+  // per row: the D requests, the request in the GPU dim (0 if none) and the
+  // affinity domain (0xFFFFFFFF = none: no node has that domain)
+  __shared__ uint32_t sq[kScoreMaxRows][D + 2];
   const int N = sp.N;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int tile0 = blockIdx.x * (256 * NPL) + wave * (64 * NPL);
@@ -244,64 +248,72 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
   const int r0 = blockIdx.y * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
   const int g = sp.gpu_dim;
-  for (int i = threadIdx.x; i < (r1 - r0) * (D + 1); i += blockDim.x) {
-    const int rr = i / (D + 1), d = i % (D + 1);
-    const int dd = d < D ? d : g;
-    sq[rr][d] = dd >= 0 ? (uint32_t)q[(int64_t)dd * qstride + rows_unit[r0 + rr]] : 0u;
+  for (int i = threadIdx.x; i < (r1 - r0) * (D + 2); i += blockDim.x) {
+    const int rr = i / (D + 2), d = i % (D + 2);
+    const int32_t unit = rows_unit[r0 + rr];
+    uint32_t v;
+    if (d == D + 1) {
+      v = (uint32_t)uaff[unit];
+    } else {
+      const int dd = d < D ? d : g;
+      v = dd >= 0 ? (uint32_t)q[(int64_t)dd * qstride + unit] : 0u;
+    }
+    sq[rr][d] = v;
   }
-  uint32_t f_[NPL][D], u_[NPL][D], rl_[NPL][D], rh_[NPL][D], fg_[NPL];
+  uint32_t f_[NPL][D], u_[NPL][D], c_[NPL][D], R_[NPL][D], k_[NPL][D], fg_[NPL], tp_[NPL];
   int32_t b_[NPL];
   bool v_[NPL];
+  bool anyW[D], allE[D];
   {
     const typename V::T *pv = reinterpret_cast<const typename V::T *>(np);
     const int64_t PV = P / NPL, iv = nb / NPL;  // P % 1024 == 0: the tile is inside
-    typename V::T pl[4 * D + 1];
+    typename V::T pl[4 * D + 2];
 #pragma unroll
-    for (int i = 0; i < 4 * D + 1; ++i) pl[i] = pv[i * PV + iv];
+    for (int i = 0; i < 4 * D + 2; ++i) pl[i] = pv[i * PV + iv];
+    uint32_t wmode[D], nonE[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) wmode[d] = nonE[d] = 0;
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         f_[k][d] = V::at(pl[4 * d], k);
         u_[k][d] = V::at(pl[4 * d + 1], k);
-        rl_[k][d] = V::at(pl[4 * d + 2], k);
-        rh_[k][d] = V::at(pl[4 * d + 3], k);
+        R_[k][d] = V::at(pl[4 * d + 2], k);
+        const uint32_t K = V::at(pl[4 * d + 3], k);
+        k_[k][d] = K & 63u;
+        const uint32_t c = f_[k][d] + u_[k][d];
+        c_[k][d] = c ? c : 1u;  // cap 0: feasible x = 0, t = 0, remainder 0 < 1
+        wmode[d] |= K & kDivW;
+        nonE[d] |= (K & kDivE) ^ kDivE;
       }
       v_[k] = nb + k < N;
       b_[k] = (int32_t)V::at(pl[4 * D], k);
+      tp_[k] = V::at(pl[4 * D + 1], k);
       fg_[k] = 0xFFFFFFFFu;  // free GPUs: never equal to a request when there is no GPU dim
 #pragma unroll
       for (int d = 0; d < D; ++d)
         if (d == g) fg_[k] = f_[k][d];
     }
-  }
-  // Per dim, wave-uniform: does any node of this wave need the Rh term
-  // (Rh > 0 only where cap <= S; large-capacity dims skip the multiply)? Is
-  // every node's cap and R below 2^24 (then u+q <= cap < 2^24 on every
-  // feasible pair and ((u+q)*R) >> 32 is one full-rate v_mul_hi_u32_u24
-  // instead of a quarter-rate v_mul_hi_u32)?
-  bool need_rh[D], fast24[D];
+    // wave-uniform division form per dim: W (64-bit products) if any node
+    // of the wave needs it, E (no remainder check, MostAllocated) if all do
 #pragma unroll
-  for (int d = 0; d < D; ++d) {
-    uint32_t any = 0, wide = 0;
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      any |= rh_[k][d];
-      wide |= rh_[k][d] | (rl_[k][d] >> 24) | ((f_[k][d] + u_[k][d]) >> 24);
+    for (int d = 0; d < D; ++d) {
+      anyW[d] = __ballot(wmode[d] != 0) != 0;
+      allE[d] = __ballot(nonE[d] != 0) == 0;
     }
-    need_rh[d] = __ballot(any != 0) != 0;
-    fast24[d] = __ballot(wide != 0) == 0;
   }
   __syncthreads();
   if (tile0 >= Ns) return;  // wave-uniform, after the only barrier
   const int words = Ns >> 6;
-  const bool store_ok = nb < Ns;  // Ns % 64 == 0: then all 4 nodes are in the row
-  const int32_t wfit = sp.w_gpu_fit;
+  const bool store_ok = nb < Ns;  // Ns % 64 == 0: then all NPL nodes are in the row
+  const int32_t wfit = sp.w_gpu_fit, waff = sp.w_affinity;
+  const uint32_t S = (uint32_t)sp.S;
   for (int r = r0; r < r1; ++r) {
     uint32_t qq[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) qq[d] = sq[r - r0][d];
-    const uint32_t qg = sq[r - r0][D];
+    const uint32_t qg = sq[r - r0][D], af = sq[r - r0][D + 1];
     bool fits[NPL];
     int32_t acc[NPL];
 #pragma unroll
@@ -309,28 +321,32 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
       fits[k] = v_[k];
       acc[k] = 0;
     }
-    // dim-outer: wave-uniform branches per dim for the multiply form
+    // dim-outer: wave-uniform branches per dim for the division form
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      uint32_t uu[NPL], util[NPL];
+      uint32_t util[NPL];
 #pragma unroll
       for (int k = 0; k < NPL; ++k) {
         fits[k] &= qq[d] <= f_[k][d];
-        uu[k] = u_[k][d] + qq[d];
-      }
-      if (fast24[d]) {
-        // infeasible pairs may have uu >= 2^24 (garbage util): masked below
-#pragma unroll
-        for (int k = 0; k < NPL; ++k) util[k] = mulhi_u24(uu[k], rl_[k][d]);
-      } else {
-#pragma unroll
-        for (int k = 0; k < NPL; ++k) util[k] = __umulhi(uu[k], rl_[k][d]);
-        // 24-bit multiplies (full rate) are exact wherever the pair fits:
-        // rh > 0 only if cap <= S <= 1024, and then uu <= cap; w <= 65535
-        // and util <= S
-        if (need_rh[d]) {
-#pragma unroll
-          for (int k = 0; k < NPL; ++k) util[k] += mul_u24(uu[k], rh_[k][d]);
+        // infeasible pairs may compute garbage (operands past 24 bits,
+        // wrapped sums): masked below
+        const uint32_t x = u_[k][d] + qq[d];
+        if (anyW[d]) {
+          bool nz;
+          const uint32_t t = div_floor32(x, c_[k][d], R_[k][d], k_[k][d], S, nz);
+          util[k] = MOST ? t : t + (nz ? 1u : 0u);
+        } else {
+          uint32_t t = mul_u24(x, R_[k][d]) >> k_[k][d];
+          if (MOST && allE[d]) {
+            util[k] = t;
+          } else {
+            // r = x*S - t*c lies in [0, 2c) and c < 2^24: exact mod 2^32
+            uint32_t rr = mul_u24(x, S) - mul_u24(t, c_[k][d]);
+            const bool up = rr >= c_[k][d];
+            t += up ? 1u : 0u;
+            rr -= up ? c_[k][d] : 0u;
+            util[k] = MOST ? t : t + (rr != 0u ? 1u : 0u);
+          }
         }
       }
 #pragma unroll
@@ -339,8 +355,9 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
     int32_t sv[NPL];
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
-      // GPU-topology fit: the job takes exactly the node's free GPUs
-      const int32_t bonus = (qg != 0u && fg_[k] == qg) ? wfit : 0;
+      // GPU-topology fit: the job takes exactly the node's free GPUs;
+      // CacheStrategy shared: the node is in the job's affinity domain
+      const int32_t bonus = ((qg != 0u && fg_[k] == qg) ? wfit : 0) + (tp_[k] == af ? waff : 0);
       const int32_t s = (MOST ? acc[k] : b_[k] - acc[k]) + bonus;
       sv[k] = fits[k] ? s : KP_SCORE_INFEASIBLE;
     }
@@ -793,7 +810,8 @@ struct ScoreL {
       dim3 grid(tiles, blocks(rows, rpb));
 #define KP_SC32(M, NP)                                                                      \
   hipLaunchKernelGGL((k_score32<D, M, NP>), grid, dim3(256), 0, c->stream, sp, c->d.np32, P, q, \
-                     qstride, rows_unit, rows, rpb, c->score_min_rpb, score, mask, Ns, rows_dev)
+                     qstride, c->d.aff, rows_unit, rows, rpb, c->score_min_rpb, score, mask, Ns,  \
+                     rows_dev)
       if (sp.most_allocated) {
         if (npl == 4) KP_SC32(true, 4); else KP_SC32(true, 2);
       } else {
@@ -805,7 +823,7 @@ struct ScoreL {
       const int rpb = 32;
       dim3 grid(blocks(Ns, 256 * NPL), blocks(rows, rpb));
       hipLaunchKernelGGL((k_score<D, NPL>), grid, dim3(256), 0, c->stream, sp, c->d.cap,
-                         c->d.used, c->d.R, c->d.base, q, qstride, rows_unit, rows, rpb,
+                         c->d.used, c->d.topo, q, qstride, c->d.aff, rows_unit, rows, rpb,
                          c->score_min_rpb, score, mask, Ns, rows_dev);
     }
     KP_HIP(hipGetLastError());
@@ -823,7 +841,7 @@ int launch_prep_nodes(kp_ctx *c, int32_t S, int most_allocated, const int32_t *w
   for (int d = 0; d < KP_MAX_DIMS; ++d) sp.w[d] = w[d];
   if (c->N == 0) return KP_OK;
   hipLaunchKernelGGL(k_prep_nodes, dim3(blocks(c->N, 256)), dim3(256), 0, c->stream, c->d.cap,
-                     c->d.R, c->d.base, c->N, c->D, S, most_allocated ? 0 : 1, sp);
+                     c->d.R32, c->d.K32, c->d.base, c->N, c->D, S, most_allocated ? 0 : 1, sp);
   KP_HIP(hipGetLastError());
   return KP_OK;
 }
@@ -918,8 +936,8 @@ struct RoundStartL {
     const int64_t n = std::max<int64_t>(hi - lo, P);
     if (n <= 0) return KP_OK;
     hipLaunchKernelGGL((k_round_start<D>), dim3(blocks(n, 256)), dim3(256), 0, c->stream,
-                       c->d.status, lo, hi, flag, c->d.cap, c->d.used, c->d.R, c->d.base, c->N, P,
-                       c->d.np32);
+                       c->d.status, lo, hi, flag, c->d.cap, c->d.used, c->d.R32, c->d.K32,
+                       c->d.base, c->d.topo, c->N, P, c->d.np32);
     KP_HIP(hipGetLastError());
     return KP_OK;
   }

@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-KP_ABI_VERSION = 1
+KP_ABI_VERSION = 2
 KP_MAX_DIMS = 8
 KP_MAX_CAND = 32
 KP_MAX_GANG = 64
@@ -44,7 +44,7 @@ class Snapshot(C.Structure):
         ("J", C.c_int32), ("N", C.c_int32), ("D", C.c_int32),
         ("req", _i64p), ("cap", _i64p), ("used", _i64p),
         ("prio", _i32p), ("gang_id", _i32p), ("gang_size", _i32p),
-        ("topo_domain", _i32p),
+        ("topo_domain", _i32p), ("affinity", _i32p),
     ]
 
 
@@ -61,6 +61,7 @@ class Params(C.Structure):
         ("n_cand", C.c_int32),
         ("util_scale", C.c_int32),
         ("max_passes", C.c_int32),
+        ("w_affinity", C.c_int32),
     ]
 
 
@@ -101,6 +102,7 @@ class Timing(C.Structure):
 # must return exactly these (tests/test_abi.py checks it).
 DEFAULT_W_DIM = (1, 1, 4, 2, 1, 1, 1, 1)
 DEFAULT_TIE_SEED = 0x6B706C61  # "kpla"
+DEFAULT_W_AFFINITY = 512
 
 
 def default_params(**over) -> Params:
@@ -117,6 +119,7 @@ def default_params(**over) -> Params:
     p.n_cand = 16
     p.util_scale = 100
     p.max_passes = 16
+    p.w_affinity = DEFAULT_W_AFFINITY
     for k, v in over.items():
         if k == "w_dim":
             for d, w in enumerate(v):
@@ -131,7 +134,7 @@ def params_dict(p: Params) -> dict:
         "w_dim": list(p.w_dim), "score_mode": p.score_mode, "gpu_dim": p.gpu_dim,
         "w_gpu_fit": p.w_gpu_fit, "w_spread": p.w_spread, "tie_mode": p.tie_mode,
         "tie_seed": p.tie_seed, "max_rounds": p.max_rounds, "n_cand": p.n_cand,
-        "util_scale": p.util_scale, "max_passes": p.max_passes,
+        "util_scale": p.util_scale, "max_passes": p.max_passes, "w_affinity": p.w_affinity,
     }
 
 
@@ -155,13 +158,15 @@ def load_library(path: str | None = None) -> C.CDLL:
     sigs = {
         "kp_params_default": (None, [C.POINTER(Params)]),
         "kp_create": (C.c_int, [C.POINTER(vp), C.POINTER(Config)]),
+        "kp_create_multi": (C.c_int, [C.POINTER(vp), _i32p, C.c_int32, C.POINTER(Config)]),
+        "kp_last_error": (C.c_char_p, [vp]),
         "kp_destroy": (None, [vp]),
         "kp_strerror": (C.c_char_p, [C.c_int]),
         "kp_abi_version": (C.c_int, []),
         "kp_dist_unique_id": (C.c_int, [vp]),
         "kp_place": (C.c_int, [vp, C.POINTER(Snapshot), C.POINTER(Params), C.POINTER(Result)]),
         "kp_load_nodes": (C.c_int, [vp, C.c_int32, C.c_int32, _i64p, _i64p, _i32p]),
-        "kp_load_jobs": (C.c_int, [vp, C.c_int32, _i64p, _i32p, _i32p, _i32p]),
+        "kp_load_jobs": (C.c_int, [vp, C.c_int32, _i64p, _i32p, _i32p, _i32p, _i32p]),
         "kp_solve": (C.c_int, [vp, C.POINTER(Params), C.POINTER(Result)]),
         "kp_fetch": (C.c_int, [vp, C.POINTER(Result)]),
         "kp_apply_delta": (C.c_int, [vp, _i32p, _i64p, C.c_int32]),
@@ -183,7 +188,8 @@ def load_library(path: str | None = None) -> C.CDLL:
 
 # every symbol include/kplace.h declares (tests check the export table)
 EXPORTED = (
-    "kp_params_default", "kp_create", "kp_destroy", "kp_strerror",
+    "kp_params_default", "kp_create", "kp_create_multi", "kp_destroy", "kp_strerror",
+    "kp_last_error",
     "kp_abi_version", "kp_dist_unique_id", "kp_place", "kp_load_nodes",
     "kp_load_jobs", "kp_solve", "kp_fetch", "kp_apply_delta", "kp_reset_nodes", "kp_score",
     "kp_last_timing", "kp_set_profiling", "kp_parse_gpu_memory", "kp_load_running",

@@ -24,15 +24,19 @@ def lib() -> C.CDLL:
 
 
 class KPlaceError(RuntimeError):
-    def __init__(self, code: int, where: str):
+    def __init__(self, code: int, where: str, detail: str = ""):
         self.code = code
+        self.detail = detail
         msg = lib().kp_strerror(code).decode(errors="replace")
-        super().__init__(f"{where}: kplace error {code} ({msg})")
+        super().__init__(f"{where}: kplace error {code} ({msg})" + (f": {detail}" if detail else ""))
 
 
-def _check(rc: int, where: str) -> None:
+def _check(rc: int, where: str, h=None) -> None:
     if rc != _abi.KP_OK:
-        raise KPlaceError(rc, where)
+        detail = ""
+        if h is not None and h.value:
+            detail = lib().kp_last_error(h).decode(errors="replace")
+        raise KPlaceError(rc, where, detail)
 
 
 def _ptr(a, t):
@@ -61,10 +65,12 @@ class Placer:
 
     def __init__(self, device: int = 0, world_size: int = 1, rank: int = 0,
                  nccl_id: bytes | None = None, max_pairs_matrix: int = 0,
-                 allgather=None):
+                 allgather=None, gpu_ids=None):
         """`allgather` (multi-process without RCCL): a callable taking this
         rank's bytes and returning every rank's bytes concatenated in rank
-        order (kp_set_allgather)."""
+        order (kp_set_allgather). `gpu_ids` (a list): one context over
+        several GPUs of this process (kp_create_multi); device / world_size /
+        rank / nccl_id are then unused."""
         cfg = _abi.Config()
         cfg.device = device
         cfg.world_size = world_size
@@ -75,7 +81,12 @@ class Placer:
             cfg.nccl_id = C.cast(self._id, C.c_void_p)
         cfg.max_pairs_matrix = max_pairs_matrix
         h = C.c_void_p()
-        _check(lib().kp_create(C.byref(h), C.byref(cfg)), "kp_create")
+        if gpu_ids is not None:
+            ids = np.ascontiguousarray(gpu_ids, dtype=np.int32)
+            _check(lib().kp_create_multi(C.byref(h), _ptr(ids, C.c_int32), ids.size,
+                                         C.byref(cfg)), "kp_create_multi")
+        else:
+            _check(lib().kp_create(C.byref(h), C.byref(cfg)), "kp_create")
         self._h = h
         self.J = self.N = self.D = 0
         self._cb = None
@@ -90,7 +101,11 @@ class Placer:
                 except Exception:  # never unwind through the C frames
                     return 1
             self._cb = _abi.ALLGATHER_FN(_cb)
-            _check(lib().kp_set_allgather(self._h, self._cb, None), "kp_set_allgather")
+            _check(lib().kp_set_allgather(self._h, self._cb, None), "kp_set_allgather", self._h)
+
+    def last_error(self) -> str:
+        """kp_last_error: detail of the last failed call on this context."""
+        return lib().kp_last_error(self._h).decode(errors="replace")
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -116,21 +131,23 @@ class Placer:
         used = _c(used, np.int64)
         topo = _c(topo, np.int32)
         _check(lib().kp_load_nodes(self._h, N, D, _ptr(cap, C.c_int64), _ptr(used, C.c_int64),
-                                   _ptr(topo, C.c_int32)), "kp_load_nodes")
+                                   _ptr(topo, C.c_int32)), "kp_load_nodes", self._h)
         self.N, self.D = N, D
 
-    def load_jobs(self, req, prio=None, gang_id=None, gang_size=None) -> None:
+    def load_jobs(self, req, prio=None, gang_id=None, gang_size=None, affinity=None) -> None:
         req = _c(req, np.int64)
         J = req.shape[1]
         prio, gang_id, gang_size = _c(prio, np.int32), _c(gang_id, np.int32), _c(gang_size, np.int32)
+        affinity = _c(affinity, np.int32)
         _check(lib().kp_load_jobs(self._h, J, _ptr(req, C.c_int64), _ptr(prio, C.c_int32),
-                                  _ptr(gang_id, C.c_int32), _ptr(gang_size, C.c_int32)),
-               "kp_load_jobs")
+                                  _ptr(gang_id, C.c_int32), _ptr(gang_size, C.c_int32),
+                                  _ptr(affinity, C.c_int32)),
+               "kp_load_jobs", self._h)
         self.J = J
 
     def solve(self, params: _abi.Params) -> dict:
         r = _abi.Result()
-        _check(lib().kp_solve(self._h, C.byref(params), C.byref(r)), "kp_solve")
+        _check(lib().kp_solve(self._h, C.byref(params), C.byref(r)), "kp_solve", self._h)
         return dict(rounds=r.rounds, passes=r.passes, placed=r.placed_jobs,
                     unplaced=r.unplaced_jobs, units=r.units, pairs=r.pairs_scored)
 
@@ -141,7 +158,7 @@ class Placer:
         used = np.empty((self.D, self.N), np.int64) if want_used else None
         r = _abi.Result(_ptr(node, C.c_int32), _ptr(score, C.c_int32), _ptr(status, C.c_int32),
                         _ptr(used, C.c_int64))
-        _check(lib().kp_fetch(self._h, C.byref(r)), "kp_fetch")
+        _check(lib().kp_fetch(self._h, C.byref(r)), "kp_fetch", self._h)
         return dict(node=node, score=score, status=status, used=used, rounds=r.rounds,
                     passes=r.passes, placed=r.placed_jobs, unplaced=r.unplaced_jobs,
                     units=r.units, pairs=r.pairs_scored)
@@ -151,7 +168,7 @@ class Placer:
         delta = _c(delta, np.int64)
         K = node_idx.shape[0]
         _check(lib().kp_apply_delta(self._h, _ptr(node_idx, C.c_int32), _ptr(delta, C.c_int64), K),
-               "kp_apply_delta")
+               "kp_apply_delta", self._h)
 
     def load_running(self, node, req, prio) -> None:
         """kp_load_running: the victim pool (running jobs) of the resident
@@ -159,7 +176,7 @@ class Placer:
         node, req, prio = _c(node, np.int32), _c(req, np.int64), _c(prio, np.int32)
         R = node.shape[0]
         _check(lib().kp_load_running(self._h, R, _ptr(node, C.c_int32), _ptr(req, C.c_int64),
-                                     _ptr(prio, C.c_int32)), "kp_load_running")
+                                     _ptr(prio, C.c_int32)), "kp_load_running", self._h)
 
     def preempt(self) -> dict:
         """kp_preempt after a solve: per-job nominated node / victims / cost."""
@@ -167,27 +184,27 @@ class Placer:
         vict = np.empty(self.J, np.int32)
         cost = np.empty(self.J, np.int64)
         r = _abi.Preemption(_ptr(node, C.c_int32), _ptr(vict, C.c_int32), _ptr(cost, C.c_int64))
-        _check(lib().kp_preempt(self._h, C.byref(r)), "kp_preempt")
+        _check(lib().kp_preempt(self._h, C.byref(r)), "kp_preempt", self._h)
         return dict(node=node, victims=vict, cost=cost, preemptors=r.preemptors,
                     nominated=r.nominated, pairs=r.pairs_scored)
 
     def reset_nodes(self) -> None:
-        _check(lib().kp_reset_nodes(self._h), "kp_reset_nodes")
+        _check(lib().kp_reset_nodes(self._h), "kp_reset_nodes", self._h)
 
     def score(self, params: _abi.Params, lo: int, hi: int):
         rows = hi - lo
         sc = np.empty((rows, self.N), np.int32)
         mk = np.empty((rows, (self.N + 63) // 64), np.uint64)
         _check(lib().kp_score(self._h, C.byref(params), lo, hi, _ptr(sc, C.c_int32),
-                              _ptr(mk, C.c_uint64)), "kp_score")
+                              _ptr(mk, C.c_uint64)), "kp_score", self._h)
         return sc, mk
 
     def set_profiling(self, on: bool) -> None:
-        _check(lib().kp_set_profiling(self._h, 1 if on else 0), "kp_set_profiling")
+        _check(lib().kp_set_profiling(self._h, 1 if on else 0), "kp_set_profiling", self._h)
 
     def timing(self) -> dict:
         t = _abi.Timing()
-        _check(lib().kp_last_timing(self._h, C.byref(t)), "kp_last_timing")
+        _check(lib().kp_last_timing(self._h, C.byref(t)), "kp_last_timing", self._h)
         return {k: getattr(t, k) for k, _ in _abi.Timing._fields_}
 
     # ---- one-shot ----------------------------------------------------------
@@ -199,16 +216,17 @@ class Placer:
         N = cap.shape[1]
         used, prio = _c(w.used, np.int64), _c(w.prio, np.int32)
         gid, gsz, topo = _c(w.gang_id, np.int32), _c(w.gang_size, np.int32), _c(w.topo, np.int32)
+        aff = _c(getattr(w, "affinity", None), np.int32)
         snap = _abi.Snapshot(J, N, D, _ptr(req, C.c_int64), _ptr(cap, C.c_int64),
                              _ptr(used, C.c_int64), _ptr(prio, C.c_int32), _ptr(gid, C.c_int32),
-                             _ptr(gsz, C.c_int32), _ptr(topo, C.c_int32))
+                             _ptr(gsz, C.c_int32), _ptr(topo, C.c_int32), _ptr(aff, C.c_int32))
         node = np.empty(J, np.int32)
         score = np.empty(J, np.int32)
         status = np.empty(J, np.int32)
         used_out = np.empty((D, N), np.int64)
         r = _abi.Result(_ptr(node, C.c_int32), _ptr(score, C.c_int32), _ptr(status, C.c_int32),
                         _ptr(used_out, C.c_int64))
-        _check(lib().kp_place(self._h, C.byref(snap), C.byref(params), C.byref(r)), "kp_place")
+        _check(lib().kp_place(self._h, C.byref(snap), C.byref(params), C.byref(r)), "kp_place", self._h)
         self.J, self.N, self.D = J, N, D
         return dict(node=node, score=score, status=status, used=used_out, rounds=r.rounds,
                     passes=r.passes, placed=r.placed_jobs, unplaced=r.unplaced_jobs,

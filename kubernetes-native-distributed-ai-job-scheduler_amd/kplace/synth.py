@@ -64,10 +64,12 @@ class Workload:
     topo: np.ndarray         # int32 [N]
     name: str = ""
     meta: dict = field(default_factory=dict)
+    affinity: np.ndarray | None = None  # int32 [J] preferred topo domain, -1 = none
 
     def arrays(self):
         return dict(req=self.req, cap=self.cap, used=self.used, prio=self.prio,
-                    gang_id=self.gang_id, gang_size=self.gang_size, topo=self.topo)
+                    gang_id=self.gang_id, gang_size=self.gang_size, topo=self.topo,
+                    affinity=self.affinity)
 
 
 def make_nodes(seed: int, N: int, ab_only: bool) -> tuple[np.ndarray, np.ndarray]:

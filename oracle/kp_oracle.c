@@ -28,8 +28,6 @@ struct kpo_state {
   const int64_t *cap;
   int64_t *used;      /* [D*N] committed usage                               */
   int32_t *topo;      /* [N]                                                 */
-  uint64_t *R;        /* [D*N] floor(S * 2^32 / cap), 0 if cap == 0 (§2.3)   */
-  int64_t *base;      /* [N]   LeastAllocated base, 0 for MostAllocated      */
   /* units in rank order (§2.2) */
   int32_t U;
   int32_t *leader;    /* [U] first job index                                 */
@@ -37,6 +35,7 @@ struct kpo_state {
   uint32_t *salt;     /* [U] rotated tie-break salt (§2.3)                   */
   int32_t *status;    /* [U] ACTIVE / PLACED / NO_FIT                        */
   int32_t *prio;      /* [U] unit priority                                   */
+  int32_t *aff;       /* [U] affinity topo domain, -1 = none (§2.3)          */
   int32_t *job_node;  /* [J]                                                 */
   int32_t *job_score; /* [J]                                                 */
   int32_t rounds;
@@ -61,6 +60,7 @@ static int check_params(const kp_params *p, int32_t D) {
   if (p->n_cand < 1 || p->n_cand > KP_MAX_CAND) return KP_EINVAL;
   if (p->util_scale < 1 || p->util_scale > 1024) return KP_EINVAL;
   if (p->max_passes < 1 || p->max_passes > 64) return KP_EINVAL;
+  if (p->w_affinity < 0 || p->w_affinity > (1 << 20)) return KP_EINVAL;
   return KP_OK;
 }
 
@@ -92,25 +92,43 @@ static uint32_t tie_key(const kpo_state *st, int32_t u, int32_t n) {
 }
 
 /* ---- §2.3 filter + score ---------------------------------------------------
- * S(q | n, base_used): the score of one more copy of request q on node n when
- * the node's usage is base_used (a D-vector); -1 if it does not fit. */
-static int64_t score_at(const kpo_state *st, const int64_t *q, int32_t n,
+ * Per dim with cap c > 0 and x = used + q <= c, exactly as kube-scheduler's
+ * NodeResourcesFit scorers compute one resource (k8s.io/kubernetes
+ * pkg/scheduler/framework/plugins/noderesources, not vendored by the
+ * reference):
+ *   MostAllocated  (mostRequestedScore):  util = floor(x * S / c)
+ *   LeastAllocated (leastRequestedScore): util = floor((c - x) * S / c)
+ * with S = util_scale (MaxNodeScore = 100 by default); cap-0 dims are
+ * skipped as kube-scheduler skips zero allocatable. The node score is the
+ * weighted SUM over dims (kube-scheduler divides it by the weight sum; see
+ * DESIGN.md §2.3 for why the numerator is kept). x * S needs up to 67 bits:
+ * 128-bit integer arithmetic, no reciprocal. */
+static int64_t util_of(int64_t x, int64_t c, int64_t S, int most) {
+  const unsigned __int128 n = (unsigned __int128)(uint64_t)x * (uint64_t)S;
+  if (most) return (int64_t)(n / (uint64_t)c);
+  const unsigned __int128 m = (unsigned __int128)(uint64_t)(c - x) * (uint64_t)S;
+  return (int64_t)(m / (uint64_t)c);
+}
+
+/* S(q | n, base_used): the score of one more copy of unit u's request q on
+ * node n when the node's usage is base_used (a D-vector); -1 if it does not
+ * fit. */
+static int64_t score_at(const kpo_state *st, int32_t u, const int64_t *q, int32_t n,
                         const int64_t *base_used) {
   const int32_t D = st->D, N = st->N;
-  int64_t acc = 0;
+  const int most = st->p.score_mode == KP_SCORE_MOST_ALLOCATED;
+  int64_t s = 0;
   for (int d = 0; d < D; ++d) {
     int64_t cap = st->cap[(int64_t)d * N + n];
     int64_t used = base_used[d];
     if (q[d] > cap - used) return -1; /* filter: used + q <= cap */
-    uint64_t u = (uint64_t)(used + q[d]);
-    uint64_t util = (u * st->R[(int64_t)d * N + n]) >> 32; /* 0..S */
-    acc += (int64_t)st->p.w_dim[d] * (int64_t)util;
+    if (cap > 0) s += (int64_t)st->p.w_dim[d] * util_of(used + q[d], cap, st->p.util_scale, most);
   }
-  int64_t s = st->p.score_mode == KP_SCORE_MOST_ALLOCATED ? acc
-                                                           : st->base[n] - acc;
   int g = st->p.gpu_dim;
   if (g >= 0 && q[g] > 0 && st->cap[(int64_t)g * N + n] - base_used[g] - q[g] == 0)
     s += st->p.w_gpu_fit; /* exact fill of the node's free GPUs */
+  if (st->aff[u] >= 0 && st->topo[n] == st->aff[u])
+    s += st->p.w_affinity; /* CacheStrategy shared: the coordinator's domain */
   return s;
 }
 
@@ -135,7 +153,7 @@ static int cmp_i32(const void *a, const void *b) {
 
 void kpo_state_free(kpo_state *st) {
   if (!st) return;
-  free(st->used); free(st->topo); free(st->R); free(st->base);
+  free(st->used); free(st->topo); free(st->aff);
   free(st->leader); free(st->size); free(st->salt);
   free(st->status); free(st->prio); free(st->job_node); free(st->job_score);
   free(st);
@@ -158,28 +176,19 @@ int kpo_state_new(const kp_snapshot *s, const kp_params *p, kpo_state **out) {
   if (!st) return KP_ENOMEM;
   st->J = J; st->N = N; st->D = D; st->p = *p;
   st->req = s->req; st->cap = s->cap;
-  int32_t *uleader, *usize, *uprio;
+  int32_t *uleader, *usize, *uprio, *uaff;
   XALLOC(st->used, (size_t)D * N, int64_t); XALLOC(st->topo, N, int32_t);
-  XALLOC(st->R, (size_t)D * N, uint64_t); XALLOC(st->base, N, int64_t);
+
   XALLOC(st->job_node, J, int32_t); XALLOC(st->job_score, J, int32_t);
   XALLOC(uleader, J, int32_t); XALLOC(usize, J, int32_t); XALLOC(uprio, J, int32_t);
-  if (!st->used || !st->topo || !st->R || !st->base || !st->job_node ||
-      !st->job_score || !uleader || !usize || !uprio) {
-    free(uleader); free(usize); free(uprio); kpo_state_free(st);
+  XALLOC(uaff, J, int32_t);
+  if (!st->used || !st->topo || !st->job_node ||
+      !st->job_score || !uleader || !usize || !uprio || !uaff) {
+    free(uleader); free(usize); free(uprio); free(uaff); kpo_state_free(st);
     return KP_ENOMEM;
   }
-  const uint64_t S = (uint64_t)p->util_scale;
-  for (int64_t i = 0; i < (int64_t)D * N; ++i) {
-    st->used[i] = s->used ? s->used[i] : 0;
-    st->R[i] = s->cap[i] > 0 ? (S << 32) / (uint64_t)s->cap[i] : 0;
-  }
-  for (int32_t n = 0; n < N; ++n) {
-    st->topo[n] = s->topo_domain ? s->topo_domain[n] : n;
-    int64_t b = 0;
-    for (int d = 0; d < D; ++d)
-      if (s->cap[(int64_t)d * N + n] > 0) b += (int64_t)p->w_dim[d] * (int64_t)S;
-    st->base[n] = p->score_mode == KP_SCORE_LEAST_ALLOCATED ? b : 0;
-  }
+  for (int64_t i = 0; i < (int64_t)D * N; ++i) st->used[i] = s->used ? s->used[i] : 0;
+  for (int32_t n = 0; n < N; ++n) st->topo[n] = s->topo_domain ? s->topo_domain[n] : n;
   for (int32_t j = 0; j < J; ++j) { st->job_node[j] = -1; st->job_score[j] = KP_SCORE_NONE; }
 
   /* units: maximal runs of equal gang_id >= 0; gang_id < 0 stands alone */
@@ -194,10 +203,13 @@ int kpo_state_new(const kp_snapshot *s, const kp_params *p, kpo_state **out) {
     for (int32_t k = j; k < e && !rc; ++k) {
       if (s->gang_size && s->gang_size[k] != len) rc = KP_EINVAL;
       if (s->prio && s->prio[k] != s->prio[j]) rc = KP_EINVAL;
+      if (s->affinity && s->affinity[k] != s->affinity[j]) rc = KP_EINVAL;
+      if (s->affinity && s->affinity[k] < -1) rc = KP_EINVAL;
       for (int d = 0; d < D && !rc; ++d)
         if (s->req[(int64_t)d * J + k] != s->req[(int64_t)d * J + j]) rc = KP_EINVAL;
     }
     uleader[U] = j; usize[U] = len; uprio[U] = s->prio ? s->prio[j] : 0;
+    uaff[U] = s->affinity ? s->affinity[j] : -1;
     ++U;
     j = e;
   }
@@ -211,7 +223,7 @@ int kpo_state_new(const kp_snapshot *s, const kp_params *p, kpo_state **out) {
       if (ids[i] == ids[i - 1]) rc = KP_EINVAL;
     free(ids);
   }
-  if (rc) { free(uleader); free(usize); free(uprio); kpo_state_free(st); return rc; }
+  if (rc) { free(uleader); free(usize); free(uprio); free(uaff); kpo_state_free(st); return rc; }
 
   /* rank order: prio desc, leader (job index) asc */
   int32_t *ord;
@@ -222,14 +234,15 @@ int kpo_state_new(const kp_snapshot *s, const kp_params *p, kpo_state **out) {
   st->U = U;
   XALLOC(st->leader, U, int32_t); XALLOC(st->size, U, int32_t);
   XALLOC(st->salt, U, uint32_t); XALLOC(st->status, U, int32_t);
-  XALLOC(st->prio, U, int32_t);
+  XALLOC(st->prio, U, int32_t); XALLOC(st->aff, U, int32_t);
   for (int32_t r = 0; r < U; ++r) {
     int32_t u = ord[r];
     st->leader[r] = uleader[u]; st->size[r] = usize[u]; st->prio[r] = uprio[u];
+    st->aff[r] = uaff[u];
     st->salt[r] = fmix32((uint32_t)uleader[u] ^ p->tie_seed);
     st->status[r] = ACTIVE;
   }
-  free(ord); free(uleader); free(usize); free(uprio);
+  free(ord); free(uleader); free(usize); free(uprio); free(uaff);
   *out = st;
   return KP_OK;
 }
@@ -269,7 +282,7 @@ int kpo_round_candidates(const kpo_state *st, int32_t unit_lo, int32_t unit_hi,
     int nc = 0;
     for (int32_t n = 0; n < N; ++n) {
       node_used(st, st->used, n, bu);
-      int64_t s = score_at(st, q, n, bu);
+      int64_t s = score_at(st, u, q, n, bu);
       if (s < 0) continue;
       uint32_t k = tie_key(st, u, n);
       int pos = nc;
@@ -315,7 +328,7 @@ static int plan_unit(const kpo_state *st, int32_t u, const int32_t *cn,
     for (int c = 0; c < K && cn[c] >= 0; ++c) {
       node_used(st, cur, cn[c], bu);
       for (int d = 0; d < D; ++d) bu[d] += planned[c] * q[d];
-      int64_t s = score_at(st, q, cn[c], bu);
+      int64_t s = score_at(st, u, q, cn[c], bu);
       if (s < 0) continue;
       int64_t dom = 0;
       for (int c2 = 0; c2 < K && cn[c2] >= 0; ++c2)
@@ -331,7 +344,7 @@ static int plan_unit(const kpo_state *st, int32_t u, const int32_t *cn,
     if (!planned[c]) continue;
     node_used(st, cur, cn[c], bu);
     out[np].unit = u; out[np].node = cn[c]; out[np].count = (int32_t)planned[c];
-    out[np].member_off = off; out[np].score = (int32_t)score_at(st, q, cn[c], bu);
+    out[np].member_off = off; out[np].score = (int32_t)score_at(st, u, q, cn[c], bu);
     off += (int32_t)planned[c];
     ++np;
   }
@@ -472,7 +485,7 @@ int kpo_score(const kp_snapshot *s, const kp_params *p, int32_t job_lo,
     if (mask) memset(mask + row * words, 0, (size_t)words * sizeof(uint64_t));
     for (int32_t n = 0; n < N; ++n) {
       node_used(st, st->used, n, bu);
-      int64_t sc = score_at(st, q, n, bu);
+      int64_t sc = score_at(st, j, q, n, bu); /* unit j = job j: no gangs/prio */
       if (score) score[row * N + n] = sc < 0 ? KP_SCORE_INFEASIBLE : (int32_t)sc;
       if (mask && sc >= 0) mask[row * words + n / 64] |= (uint64_t)1 << (n % 64);
     }

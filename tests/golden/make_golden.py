@@ -35,6 +35,7 @@ def save(name, w, p):
     pd = _abi.params_dict(p)
     arrs = dict(req=w.req, cap=w.cap, used=w.used, prio=w.prio, gang_id=w.gang_id,
                 gang_size=w.gang_size, topo=w.topo,
+                **({} if w.affinity is None else {"affinity": w.affinity}),
                 out_node=r["node"], out_score=r["score"], out_status=r["status"],
                 out_used=r["used"], out_rounds=np.int64(r["rounds"]),
                 out_passes=np.int64(r["passes"]))
@@ -92,6 +93,16 @@ def main():
          _abi.default_params(n_cand=1, max_passes=1, util_scale=1024))
     save("config2_small", synth.config2(2000, 200), _abi.default_params(**synth.CONFIG_PARAMS[2]))
     save("config3_small", synth.config3(2000, 160), _abi.default_params(**synth.CONFIG_PARAMS[3]))
+    w = random_workload(1003, J=500, N=96)
+    rng = np.random.default_rng(1003)
+    gid = w.gang_id
+    aff = rng.integers(-1, 96 // 5, size=w.J).astype(np.int32)
+    for g in np.unique(gid[gid >= 0]):  # one domain per gang
+        aff[gid == g] = aff[gid == g][0]
+    w.affinity = aff
+    save("rand3_affinity", w, _abi.default_params(w_affinity=300))
+    save("rand4_least_scale", random_workload(1004, J=400, N=77),
+         _abi.default_params(score_mode=1, util_scale=1023))
     sample_crs()
 
 

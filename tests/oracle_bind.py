@@ -69,7 +69,7 @@ class SnapshotBuf:
     """Keeps contiguous numpy arrays alive behind a kp_snapshot."""
 
     def __init__(self, req, cap, used=None, prio=None, gang_id=None, gang_size=None,
-                 topo=None):
+                 topo=None, affinity=None):
         req = np.ascontiguousarray(req, dtype=np.int64)
         cap = np.ascontiguousarray(cap, dtype=np.int64)
         self.D, self.J = req.shape
@@ -82,16 +82,19 @@ class SnapshotBuf:
             gang_id=None if gang_id is None else np.ascontiguousarray(gang_id, dtype=np.int32),
             gang_size=None if gang_size is None else np.ascontiguousarray(gang_size, dtype=np.int32),
             topo=None if topo is None else np.ascontiguousarray(topo, dtype=np.int32),
+            affinity=None if affinity is None else np.ascontiguousarray(affinity, dtype=np.int32),
         )
         a = self.arrs
         self.snap = _abi.Snapshot(
             self.J, self.N, self.D, _p(a["req"], C.c_int64), _p(a["cap"], C.c_int64),
             _p(a["used"], C.c_int64), _p(a["prio"], C.c_int32), _p(a["gang_id"], C.c_int32),
-            _p(a["gang_size"], C.c_int32), _p(a["topo"], C.c_int32))
+            _p(a["gang_size"], C.c_int32), _p(a["topo"], C.c_int32),
+            _p(a["affinity"], C.c_int32))
 
     @classmethod
     def from_workload(cls, w):
-        return cls(w.req, w.cap, w.used, w.prio, w.gang_id, w.gang_size, w.topo)
+        return cls(w.req, w.cap, w.used, w.prio, w.gang_id, w.gang_size, w.topo,
+                   getattr(w, "affinity", None))
 
 
 class ResultBuf:

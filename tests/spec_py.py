@@ -20,9 +20,16 @@ def fmix32(h):
     return h
 
 
-def place(req, cap, used, prio, gang_id, topo, p):
+def util(x, c, S, most):
+    """One dimension's utilisation score, kube-scheduler's integer formulas:
+    mostRequestedScore floor(x*S/c), leastRequestedScore floor((c-x)*S/c)."""
+    return (x * S) // c if most else ((c - x) * S) // c
+
+
+def place(req, cap, used, prio, gang_id, topo, p, affinity=None):
     """req[d][j], cap[d][n], used[d][n] as nested lists / numpy; p = dict of
-    kp_params fields. Returns dict(node, score, status, used, rounds, passes)."""
+    kp_params fields; affinity[j] = preferred topo domain or -1. Returns
+    dict(node, score, status, used, rounds, passes)."""
     D = len(cap)
     N = len(cap[0]) if D else 0
     J = len(req[0]) if D else 0
@@ -31,10 +38,9 @@ def place(req, cap, used, prio, gang_id, topo, p):
     req = [[int(x) for x in row] for row in req]
     topo = [int(t) for t in topo] if topo is not None else list(range(N))
     S = p["util_scale"]
-    R = [[(S << 32) // c if c > 0 else 0 for c in cap[d]] for d in range(D)]
     w = p["w_dim"]
-    base = [sum(w[d] * S for d in range(D) if cap[d][n] > 0)
-            if p["score_mode"] == 1 else 0 for n in range(N)]
+    most = p["score_mode"] == 0
+    aff_j = [int(a) for a in affinity] if affinity is not None else [-1] * J
 
     # §2.2 units
     units = []  # (leader, size, prio)
@@ -45,7 +51,7 @@ def place(req, cap, used, prio, gang_id, topo, p):
         if g >= 0:
             while e < J and gang_id[e] == g:
                 e += 1
-        units.append((j, e - j, int(prio[j]) if prio is not None else 0))
+        units.append((j, e - j, int(prio[j]) if prio is not None else 0, aff_j[j]))
         j = e
     units.sort(key=lambda u: (-u[2], u[0]))
     U = len(units)
@@ -54,16 +60,19 @@ def place(req, cap, used, prio, gang_id, topo, p):
     job_node = [-1] * J
     job_score = [-1] * J
 
-    def S_(q, n, bu):
-        acc = 0
+    def S_(u, q, n, bu):
+        s = 0
         for d in range(D):
             if q[d] > cap[d][n] - bu[d]:
                 return -1
-            acc += w[d] * (((bu[d] + q[d]) * R[d][n]) >> 32)
-        s = acc if p["score_mode"] == 0 else base[n] - acc
+            if cap[d][n] > 0:
+                s += w[d] * util(bu[d] + q[d], cap[d][n], S, most)
         g = p["gpu_dim"]
         if g >= 0 and q[g] > 0 and cap[g][n] - bu[g] - q[g] == 0:
             s += p["w_gpu_fit"]
+        a = units[u][3]
+        if a >= 0 and topo[n] == a:
+            s += p.get("w_affinity", 0)
         return s
 
     def tie(u, n):
@@ -83,7 +92,7 @@ def place(req, cap, used, prio, gang_id, topo, p):
             if status[u] != "A":
                 continue
             q = q_of(u)
-            scored = [(S_(q, n, [used[d][n] for d in range(D)]), n) for n in range(N)]
+            scored = [(S_(u, q, n, [used[d][n] for d in range(D)]), n) for n in range(N)]
             scored = [(s, n) for s, n in scored if s >= 0]
             scored.sort(key=lambda t: (-t[0], tie(u, t[1])))
             cands[u] = [n for _, n in scored[:K]]
@@ -101,7 +110,7 @@ def place(req, cap, used, prio, gang_id, topo, p):
                     best = None
                     for c, n in enumerate(cl):
                         bu = [used[d][n] + planned[c] * q[d] for d in range(D)]
-                        s = S_(q, n, bu)
+                        s = S_(u, q, n, bu)
                         if s < 0:
                             continue
                         dom = sum(planned[c2] for c2 in range(len(cl)) if topo[cl[c2]] == topo[n])
@@ -121,7 +130,7 @@ def place(req, cap, used, prio, gang_id, topo, p):
                 for c, n in enumerate(cl):
                     if planned[c]:
                         props.append((n, u, planned[c], off,
-                                      S_(q, n, [used[d][n] for d in range(D)])))
+                                      S_(u, q, n, [used[d][n] for d in range(D)])))
                         off += planned[c]
             if not props:
                 break
@@ -153,7 +162,7 @@ def place(req, cap, used, prio, gang_id, topo, p):
         rounds += 1
     code = {"P": 0, "F": 1, "A": 2}
     out_status = [0] * J
-    for u, (ld, sz, _) in enumerate(units):
+    for u, (ld, sz, _, _a) in enumerate(units):
         for m in range(sz):
             out_status[ld + m] = code[status[u]]
             if status[u] != "P":

@@ -497,3 +497,182 @@ def test_config1_runner_gpu(oracle, placer):
                            for c in v["conditions"]] for k, v in d.items()}
     assert strip(got) == strip(want)
     assert (s_gpu["placed"], s_gpu["rounds"]) == (s_cpu["placed"], s_cpu["rounds"])
+
+
+# ---------------------------------------------------------------------------
+# exact utilisation at the boundaries: every division form of
+# k_score32 (E / C / W waves, mixed waves) and of the 64-bit path
+# ---------------------------------------------------------------------------
+def boundary_nodes(rng, N, top):
+    """Caps across the division modes; usage so that x = used + q hits
+    {cap, cap - 1, 1, 0, random} for the probe requests."""
+    kinds = rng.integers(0, 5, size=N)
+    cap = np.where(kinds == 0, rng.integers(0, 4096, size=N),
+                   np.where(kinds == 1, rng.integers(4096, 1 << 24, size=N),
+                            np.where(kinds == 2, rng.integers(1 << 24, 1 << top, size=N),
+                                     np.where(kinds == 3, (1 << rng.integers(1, top, size=N)) - 1,
+                                              1 << rng.integers(0, top - 1, size=N)))))
+    cap[: N // 2] = rng.integers(1, 1 << 24, size=N // 2)  # whole fast waves too
+    return cap.astype(np.int64)
+
+
+@pytest.mark.parametrize("top,mode,scale", [(31, 0, 100), (32, 1, 100), (32, 0, 1024),
+                                            (25, 1, 7), (50, 0, 1024), (56, 1, 100)])
+def test_score_matrix_boundaries(oracle, placer, top, mode, scale):
+    rng = np.random.default_rng(top * 10 + mode)
+    D, N = 2, 1400
+    cap = np.stack([boundary_nodes(rng, N, min(top, 56)) for _ in range(D)])
+    # probe q = 1 on every node; usage cap - 1, cap - 2, 0, random: x = cap,
+    # cap - 1, 1 and random after the request
+    pick = rng.integers(0, 4, size=(D, N))
+    used = np.where(pick == 0, cap - 1, np.where(pick == 1, cap - 2, np.where(
+        pick == 2, 0, (cap * rng.random((D, N))).astype(np.int64))))
+    used = np.clip(used, 0, cap)
+    req = np.ones((D, 3), np.int64)
+    req[:, 1] = 0
+    req[:, 2] = 2
+    p = _abi.default_params(score_mode=mode, util_scale=scale, gpu_dim=-1, w_dim=(3, 5))
+    placer.load_nodes(cap, used)
+    placer.load_jobs(req)
+    sc, mk = placer.score(p, 0, 3)
+    osc, omk = oracle.score(oracle.SnapshotBuf(req, cap, used), p, 0, 3)
+    bad = np.argwhere(sc != osc)
+    assert bad.size == 0, f"first mismatches {bad[:5].tolist()}: gpu {sc[tuple(bad[0])]} cpu {osc[tuple(bad[0])]}"
+    assert np.array_equal(mk, omk)
+
+
+def test_full_node_scores_S_gpu(oracle, placer):
+    a = synth.SHAPES[0].reshape(4, 1)
+    placer.load_nodes(np.repeat(a, 70, axis=1))
+    placer.load_jobs(np.repeat(a, 2, axis=1))
+    sc, _ = placer.score(_abi.default_params(w_dim=(1, 1, 4, 2), w_gpu_fit=0), 0, 2)
+    assert (sc == 800).all()
+
+
+def affinity_workload(seed, J, N):
+    w = random_workload(seed, J, N)
+    rng = np.random.default_rng(seed + 99)
+    aff = rng.integers(-1, N // 5 + 1, size=w.J).astype(np.int32)
+    for g in np.unique(w.gang_id[w.gang_id >= 0]):
+        aff[w.gang_id == g] = aff[w.gang_id == g][0]
+    w.affinity = aff
+    return w
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_place_affinity_parity(oracle, placer, seed):
+    """CacheStrategy=shared: the affinity bonus on the job's domain."""
+    w = affinity_workload(500 + seed, J=900, N=120 + 7 * seed)
+    p = _abi.default_params(w_affinity=[512, 37, 4096, 0][seed], score_mode=seed % 2,
+                            tie_mode=(seed // 2) % 2)
+    g, o = _place_both(oracle, placer, w, p)
+    _assert_same(g, o, f"affinity seed {seed}")
+    if p.w_affinity:
+        ok = (g["node"] >= 0) & (w.affinity >= 0)
+        assert (w.topo[g["node"][ok]] == w.affinity[ok]).mean() > 0.2
+
+
+def test_place_affinity_wide_parity(oracle, placer):
+    # 64-bit path (caps >= 2^32) with affinity
+    w = affinity_workload(600, J=500, N=90)
+    w.cap = w.cap * (1 << 30)
+    w.used = w.used * (1 << 30)
+    w.req = w.req * (1 << 29)
+    p = _abi.default_params(w_affinity=700)
+    g, o = _place_both(oracle, placer, w, p)
+    _assert_same(g, o, "affinity wide")
+
+
+# ---------------------------------------------------------------------------
+# the C-ABI contract for the Go host (include/kplace.h): atomic kp_place,
+# per-context error text, failed loads leave no snapshot
+# ---------------------------------------------------------------------------
+def test_place_is_atomic_across_threads(oracle):
+    """Two OS threads call kp_place on ONE context with different snapshots;
+    every result equals the oracle's for its own snapshot (no interleaving of
+    one thread's load with the other's solve)."""
+    import threading
+    ws = [synth.config3(3_000, 300), synth.config2(2_000, 250)]
+    ps = [_abi.default_params(**synth.CONFIG_PARAMS[3]), _abi.default_params(**synth.CONFIG_PARAMS[2])]
+    want = [oracle.place(_snap(oracle, w), p, nthreads=NTH) for w, p in zip(ws, ps)]
+    errors = []
+    with Placer(device=0) as pl:
+        def run(i):
+            try:
+                for _ in range(6):
+                    g = pl.place(ws[i], ps[i])
+                    for k in ("node", "score", "status", "used"):
+                        if not np.array_equal(g[k], want[i][k]):
+                            errors.append((i, k))
+            except Exception as e:  # noqa: BLE001
+                errors.append((i, repr(e)))
+        ts = [threading.Thread(target=run, args=(i,)) for i in (0, 1)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    assert not errors, errors
+
+
+def test_last_error_is_per_context_and_failed_load_unloads(placer):
+    cap = np.full((4, 3), 10, np.int64)
+    with pytest.raises(KPlaceError) as e:
+        placer.load_nodes(cap, cap + 1)
+    assert e.value.code == _abi.KP_EINVAL and "used" in e.value.detail
+    assert "used" in placer.last_error()
+    placer.load_nodes(cap)
+    placer.load_jobs(np.ones((4, 2), np.int64))
+    placer.solve(_abi.default_params())
+    assert placer.last_error() == ""
+    with pytest.raises(KPlaceError):  # a failed job load after a good one ...
+        placer.load_jobs(-np.ones((4, 5), np.int64))
+    with pytest.raises(KPlaceError) as e:  # ... leaves no queue to solve or fetch
+        placer.solve(_abi.default_params())
+    assert e.value.code == _abi.KP_ESTATE
+    with pytest.raises(KPlaceError) as e:
+        placer.fetch()
+    assert e.value.code == _abi.KP_ESTATE
+    with pytest.raises(KPlaceError):  # a failed node load drops the node table
+        placer.load_nodes(cap, -cap)
+    with pytest.raises(KPlaceError) as e:
+        placer.load_jobs(np.ones((4, 2), np.int64))
+    assert e.value.code == _abi.KP_ESTATE
+
+
+# ---------------------------------------------------------------------------
+# kp_create_multi: one context, one worker thread per shard (here several
+# shards on the one GPU of the box, exchanging in process; distinct GPUs use
+# RCCL) — bit-exact with the oracle and with the single-GPU context
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("ids,cfg", [([0, 0], (3, 8_000, 640)), ([0, 0, 0], (2, 3_000, 300)),
+                                     ([0, 0], (3, 1, 64)), ([0], (3, 4_000, 400))])
+def test_create_multi_parity(oracle, ids, cfg):
+    no, J, N = cfg
+    w = synth.config(no, J, N)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[no])
+    with Placer(gpu_ids=ids) as pl:
+        g = pl.place(w, p)
+        g2 = pl.place(w, p)
+    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
+    _assert_same(g, o, f"multi {ids}")
+    _assert_same(g2, o, f"multi {ids} again")
+
+
+def test_create_multi_streaming(oracle):
+    cap, topo, req, prio = synth.config5_trace(4_000, 1_000)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[5])
+    used_o = np.zeros_like(cap)
+    with Placer(gpu_ids=[0, 0]) as pl:
+        pl.load_nodes(cap, None, topo)
+        for b in range(4):
+            lo, hi = b * 1000, (b + 1) * 1000
+            rq = np.ascontiguousarray(req[:, lo:hi])
+            pl.load_jobs(rq, prio[lo:hi])
+            pl.solve(p)
+            g = pl.fetch()
+            o = oracle.place(oracle.SnapshotBuf(rq, cap, used_o, prio[lo:hi], topo=topo), p, NTH)
+            _assert_same(g, o, f"multi batch {b}")
+            used_o = o["used"].copy()
+            done = np.nonzero(g["node"] >= 0)[0][::3]
+            pl.apply_delta(g["node"][done], -rq[:, done])
+            np.subtract.at(used_o.T, g["node"][done], rq[:, done].T)

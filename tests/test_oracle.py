@@ -177,9 +177,10 @@ def rand_w(seed, J, N, D=3):
     prc = rng.integers(0, 3, size=len(sizes)).astype(np.int32)
     cr = np.repeat(np.arange(len(sizes)), sizes)
     gid = np.where(np.repeat(sizes, sizes) > 1, cr, -1).astype(np.int32)
+    affc = rng.integers(-1, N // 3 + 1, size=len(sizes)).astype(np.int32)  # -1 = none
     return synth.Workload(J, N, D, np.ascontiguousarray(reqc[:, cr]), cap, used, prc[cr], gid,
                           np.repeat(sizes, sizes).astype(np.int32),
-                          (np.arange(N) // 3).astype(np.int32))
+                          (np.arange(N) // 3).astype(np.int32), affinity=affc[cr])
 
 
 @pytest.mark.parametrize("seed", range(12))
@@ -187,9 +188,11 @@ def test_oracle_matches_python_spec(oracle, seed):
     w = rand_w(seed, J=40 + 7 * seed, N=6 + seed)
     p = P(w_dim=(1, 3, 2) + (1,) * 5, gpu_dim=seed % 3 - 1, w_gpu_fit=50 * (seed % 2),
           w_spread=7 * (seed % 3), tie_mode=seed % 2, score_mode=(seed // 2) % 2,
-          n_cand=1 + seed % 5, max_passes=1 + seed % 4, util_scale=[100, 16, 1024][seed % 3])
+          n_cand=1 + seed % 5, max_passes=1 + seed % 4, util_scale=[100, 16, 1024][seed % 3],
+          w_affinity=[0, 3, 40][seed % 3])
     r = run(oracle, w, p, threads=2)
-    s = spec_py.place(w.req, w.cap, w.used, w.prio, w.gang_id, w.topo, _abi.params_dict(p))
+    s = spec_py.place(w.req, w.cap, w.used, w.prio, w.gang_id, w.topo, _abi.params_dict(p),
+                      affinity=w.affinity)
     assert r["node"].tolist() == s["node"]
     assert r["score"].tolist() == s["score"]
     assert r["status"].tolist() == s["status"]
@@ -214,7 +217,8 @@ def test_score_matrix_matches_python(oracle):
     for j in range(w.J):
         for n in range(w.N):
             one = spec_py.place(w.req[:, j:j + 1], w.cap[:, n:n + 1], w.used[:, n:n + 1],
-                                None, None, None, dict(pd, max_rounds=1, max_passes=1, n_cand=1))
+                                None, None, None, dict(pd, max_rounds=1, max_passes=1, n_cand=1,
+                                                       w_affinity=0))
             want = one["score"][0]
             assert sc[j, n] == want, (j, n)
             assert bool((int(mk[j, n // 64]) >> (n % 64)) & 1) == (want >= 0)
@@ -231,7 +235,7 @@ def test_golden_fixture(oracle, path):
                                for k, v in pd.items()})
     w = synth.Workload(int(z["req"].shape[1]), int(z["cap"].shape[1]), int(z["req"].shape[0]),
                        z["req"], z["cap"], z["used"], z["prio"], z["gang_id"], z["gang_size"],
-                       z["topo"])
+                       z["topo"], affinity=z["affinity"] if "affinity" in z.files else None)
     r = run(oracle, w, p, threads=4)
     for k in ("node", "score", "status", "used"):
         assert np.array_equal(r[k], z["out_" + k]), k

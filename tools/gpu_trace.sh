@@ -1,0 +1,7 @@
+# Kernel trace of one bench solve (no per-kernel events) for per-launch analysis.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/trace${1:-}
+rm -rf $OUT; mkdir -p $OUT
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-stream --no-kernel-events > $OUT/bench.log 2>&1
+echo "rocprof rc=$?"
