@@ -5,19 +5,37 @@ A "step" is one full placement of the pending queue (100k jobs x 10k nodes,
 gangs of {1,2,4,8}, 8-GPU xGMI-island nodes) with the snapshot already
 resident in HBM: kp_reset_nodes (device copy of the loaded usage) + kp_solve
 (every filter+score pass, top-K select, acceptance pass and commit, plus the
-RCCL candidate exchange when N>1). `value` = J*N job-node pairs resolved per
-second of whole-job wall time (max over ranks); the total problem is fixed as
-N grows (strong scaling). Synthetic data (splitmix64 generator).
+candidate exchange when N>1). `value` = J*N job-node pairs resolved per second
+of whole-job wall time (max over ranks); the total problem is fixed as N grows
+(strong scaling). Synthetic data (splitmix64 generator).
+
+Beside the step (same run, outside the timed steps):
+  latency_ms      kp_place from host arrays: validate + upload the snapshot,
+                  solve, download the assignment (the headline "full-queue
+                  placement latency"; the reference's analogue is
+                  the reconcile histogram around Reconcile,
+                  internal/controller/llmservice_controller.go:70-73);
+  config4         BASELINE config #4 (200k x 20k, 30% GPU occupancy of running
+                  jobs): solve + kp_preempt;
+  streaming       BASELINE config #5 (1M-job trace, 5k micro-batches, 50k nodes);
+  cpu_baseline    the CPU restatement (oracle/, test infrastructure) on the SAME
+                  full config #3, on 1 thread and on every host core given to
+                  this job.
 
 Multi-GPU: one process per GPU (torch.distributed.run); the control plane
 (barrier, unique-id broadcast, max-reduce of times) runs on gloo, the data
-path's candidate exchange on RCCL inside libkplace.
+path's candidate exchange on RCCL inside libkplace. `--gpus N` without a
+launcher re-launches itself under torch.distributed.run (before anything
+touches a GPU); `--single-process` drives the N GPUs from this one process
+instead (kp_create_multi: one worker thread per GPU inside the library).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
+import subprocess
 import sys
 import time
 
@@ -28,33 +46,55 @@ sys.path.insert(0, PKG)
 import numpy as np  # noqa: E402
 
 from kplace import _abi, synth  # noqa: E402
-from kplace.engine import Placer, unique_id  # noqa: E402
 
 METRIC = "job-node pairs scored/sec + full-queue placement latency (100k jobs × 10k nodes)"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
-def cpu_baseline(args):
-    """Timed CPU restatement (oracle/, test infrastructure) on a bounded
-    sample of the same workload family: config #3 shrunk by `cpu_shrink` in
-    both jobs and nodes (1/shrink^2 of the pairs), full placement."""
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def host_cores() -> int:
+    """Cores this job may use: the box's share (OMP_NUM_THREADS is set to it
+    on the GPU pool; os.cpu_count() there shows the whole machine)."""
+    n = os.environ.get("OMP_NUM_THREADS")
+    return max(1, int(n)) if n and n.isdigit() else (os.cpu_count() or 1)
+
+
+def cpu_baseline(args, w, p):
+    """The CPU restatement (oracle/kp_oracle.c, OpenMP candidate phase) on the
+    same full config #3, single-threaded and on every host core."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_bind as ob
-    J, N = args.jobs // args.cpu_shrink, args.nodes // args.cpu_shrink
-    w = synth.config3(J, N)
-    p = _abi.default_params(**synth.CONFIG_PARAMS[3])
-    threads = min(16, os.cpu_count() or 1)
     sb = ob.SnapshotBuf.from_workload(w)
-    t = time.perf_counter()
-    r = ob.place(sb, p, nthreads=threads)
-    dt = time.perf_counter() - t
-    return {"value": J * N / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/kp_oracle.c full placement of config3 {J}x{N} "
-                      f"(1/{args.cpu_shrink**2} of the pairs), {r['rounds']} rounds, "
-                      f"{dt*1e3:.0f} ms, OpenMP {threads} threads"}
+    pairs = float(w.J) * w.N
+    out = {}
+    for label, threads in (("all_cores", host_cores()), ("single", 1)):
+        if label == "single" and args.cpu_single_sample < 1.0:
+            # bounded sample: the first rounds of the same solve
+            continue
+        t = time.perf_counter()
+        r = ob.place(sb, p, nthreads=threads)
+        dt = time.perf_counter() - t
+        out[label] = {"pairs_per_s": pairs / dt, "seconds": dt, "threads": threads,
+                      "rounds": r["rounds"], "placed_jobs": r["placed"]}
+    allc = out["all_cores"]
+    return {"value": allc["pairs_per_s"], "unit": "pairs/s", "cores": allc["threads"],
+            "kind": "port", "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
+            "sample": f"oracle/kp_oracle.c full placement of the same config3 {w.J}x{w.N} "
+                      f"snapshot ({allc['rounds']} rounds), OpenMP over the host cores; "
+                      f"'single' = 1 thread",
+            **out}
 
 
-def streaming(args):
+def streaming(args, make_placer):
     """BASELINE config #5: a 1M-job trace replayed in micro-batches against a
     50k-node resident table; after each batch a deterministic 20% of the
     running jobs complete (negative kp_apply_delta). Per-batch latency =
@@ -63,9 +103,9 @@ def streaming(args):
     cap, topo, req, prio = synth.config5_trace(args.stream_jobs, args.stream_nodes)
     p = _abi.default_params(**synth.CONFIG_PARAMS[5])
     B = args.stream_batch
-    lat = []
-    placed = 0
-    with Placer(device=int(os.environ.get("LOCAL_RANK", "0"))) as pl:
+    lat, parts = [], {"apply": 0.0, "load": 0.0, "solve": 0.0, "fetch": 0.0}
+    placed = rounds = 0
+    with make_placer() as pl:
         pl.load_nodes(cap, None, topo)
         run_node = np.zeros(0, np.int32)
         run_job = np.zeros(0, np.int64)
@@ -73,13 +113,20 @@ def streaming(args):
         for b in range(args.stream_jobs // B):
             lo, hi = b * B, (b + 1) * B
             rq = np.ascontiguousarray(req[:, lo:hi])
-            t = time.perf_counter()
+            t0 = time.perf_counter()
             if pend_n is not None and pend_n.size:
                 pl.apply_delta(pend_n, pend_d)
+            t1 = time.perf_counter()
             pl.load_jobs(rq, prio[lo:hi])
-            pl.solve(p)
+            t2 = time.perf_counter()
+            st = pl.solve(p)
+            t3 = time.perf_counter()
             g = pl.fetch(want_used=False)
-            lat.append(time.perf_counter() - t)
+            t4 = time.perf_counter()
+            lat.append(t4 - t0)
+            for k, a, z in (("apply", t0, t1), ("load", t1, t2), ("solve", t2, t3), ("fetch", t3, t4)):
+                parts[k] += z - a
+            rounds += st["rounds"]
             ok = g["node"] >= 0
             placed += int(ok.sum())
             run_node = np.concatenate([run_node, g["node"][ok]])
@@ -89,11 +136,57 @@ def streaming(args):
             pend_d = np.ascontiguousarray(-req[:, run_job[done]])
             run_node, run_job = run_node[~done], run_job[~done]
     lat_ms = np.array(lat) * 1e3
+    n = len(lat)
     return {"config": f"#5 streaming: {args.stream_jobs} jobs in {B}-job micro-batches vs "
                       f"{args.stream_nodes} nodes, 20% completions per batch",
-            "batches": len(lat), "p50_ms": float(np.percentile(lat_ms, 50)),
+            "batches": n, "p50_ms": float(np.percentile(lat_ms, 50)),
             "p99_ms": float(np.percentile(lat_ms, 99)), "max_ms": float(lat_ms.max()),
-            "jobs_per_s": args.stream_jobs / float(np.sum(lat)), "placed_jobs": placed}
+            "jobs_per_s": args.stream_jobs / float(np.sum(lat)), "placed_jobs": placed,
+            "mean_rounds": rounds / max(n, 1),
+            "mean_ms": {k: v * 1e3 / max(n, 1) for k, v in parts.items()}}
+
+
+def config4(args, make_placer):
+    """BASELINE config #4: 200k pending x 20k nodes pre-filled with running
+    jobs (priorities 0-3) to 30% GPU occupancy; one step = reset the resident
+    usage + solve + preemption nominations for every NO_FIT singleton."""
+    w = synth.config4(args.c4_jobs, args.c4_nodes)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[4])
+    m = w.meta
+    with make_placer() as pl:
+        pl.load_nodes(w.cap, w.used, w.topo)
+        pl.load_running(m["run_node"], m["run_req"], m["run_prio"])
+        pl.load_jobs(w.req, w.prio, w.gang_id, w.gang_size)
+        sol, pre = [], []
+        for it in range(args.c4_steps + 1):
+            pl.reset_nodes()
+            t0 = time.perf_counter()
+            st = pl.solve(p)
+            t1 = time.perf_counter()
+            pr = pl.preempt()
+            t2 = time.perf_counter()
+            if it:  # first iteration: warmup
+                sol.append(t1 - t0)
+                pre.append(t2 - t1)
+    s_ms, p_ms = 1e3 * float(np.mean(sol)), 1e3 * float(np.mean(pre))
+    return {"config": f"#4 preemption: {w.J} pending x {w.N} nodes, {m['run_node'].size} running "
+                      f"jobs at {w.used[2].sum() / w.cap[2].sum():.3f} GPU occupancy",
+            "solve_ms": s_ms, "preempt_ms": p_ms,
+            "pairs_per_s": float(w.J) * w.N / ((s_ms + p_ms) / 1e3),
+            "rounds": st["rounds"], "passes": st["passes"], "placed_jobs": st["placed"],
+            "preemptors": pr["preemptors"], "nominated": pr["nominated"],
+            "preempt_pairs": pr["pairs"], "steps": args.c4_steps}
+
+
+def relaunch_distributed(args) -> int:
+    """`--gpus N` without a launcher: run this script under
+    torch.distributed.run as N ranks (a child process; this process never
+    touches a GPU) and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(args.master_port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -103,20 +196,37 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--jobs", type=int, default=100_000)
     ap.add_argument("--nodes", type=int, default=10_000)
-    ap.add_argument("--cpu-shrink", type=int, default=4)
+    ap.add_argument("--single-process", action="store_true",
+                    help="drive --gpus N GPUs from this process (kp_create_multi)")
+    ap.add_argument("--master-port", type=int, default=29533)
+    ap.add_argument("--place-steps", type=int, default=5, help="kp_place (host->host) repetitions")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-single-sample", type=float, default=1.0,
+                    help="<1: skip the single-thread oracle run")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     ap.add_argument("--stream-jobs", type=int, default=1_000_000)
     ap.add_argument("--stream-batch", type=int, default=5_000)
     ap.add_argument("--stream-nodes", type=int, default=50_000)
     ap.add_argument("--no-stream", action="store_true")
+    ap.add_argument("--c4-jobs", type=int, default=200_000)
+    ap.add_argument("--c4-nodes", type=int, default=20_000)
+    ap.add_argument("--c4-steps", type=int, default=3)
+    ap.add_argument("--no-config4", action="store_true")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="time the steps without per-launch HIP events (no roofline)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and env_world is None and not args.single_process:
+        sys.exit(relaunch_distributed(args))
+    world = int(env_world or "1")
+    if not args.single_process and world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks; one rank per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    from kplace.engine import Placer, unique_id  # noqa: E402  (loads libkplace.so)
+
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -129,9 +239,20 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         nid = obj[0]
 
+    if args.single_process:
+        ids = list(range(args.gpus))
+        make_placer = lambda: Placer(gpu_ids=ids)  # noqa: E731
+        parallelism = f"job-row shards x{args.gpus} (one process, kp_create_multi)"
+        n_gpus = args.gpus
+    else:
+        make_placer = lambda: Placer(device=local, world_size=world, rank=rank,  # noqa: E731
+                                     nccl_id=nid)
+        parallelism = f"job-row shards x{world}"
+        n_gpus = world
+
     w = synth.config3(args.jobs, args.nodes)
     p = _abi.default_params(**synth.CONFIG_PARAMS[3])
-    pl = Placer(device=local, world_size=world, rank=rank, nccl_id=nid)
+    pl = make_placer()
     pl.load_nodes(w.cap, w.used, w.topo)
     pl.load_jobs(w.req, w.prio, w.gang_id, w.gang_size)
 
@@ -139,13 +260,21 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    def max_over_ranks(x: float) -> float:
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
     for _ in range(args.warmup):
         pl.reset_nodes()
         pl.solve(p)
     pl.set_profiling(not args.no_kernel_events)
     barrier()
     t0 = time.perf_counter()
-    score_ms = score_b = select_ms = 0.0
+    score_ms = score_b = 0.0
     launches = 0
     st = None
     for _ in range(args.steps):
@@ -154,34 +283,43 @@ def main():
         tm = pl.timing()
         score_ms += tm["score_ms"]
         score_b += tm["score_bytes"]
-        select_ms += tm["select_ms"]
         launches += tm["score_launches"]
     barrier()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = max_over_ranks(time.perf_counter() - t0)
     ms = dt * 1e3 / args.steps
+    pl.set_profiling(False)
+
+    # full-queue placement latency: snapshot in host memory -> assignment in
+    # host memory (kp_place: validate + H2D + solve + D2H), outside the steps
+    lat = []
+    for _ in range(args.place_steps):
+        barrier()
+        t = time.perf_counter()
+        pl.place(w, p)
+        lat.append(max_over_ranks(time.perf_counter() - t))
+    pl.close()
+    latency_ms = 1e3 * float(np.median(lat)) if lat else None
+
     if rank != 0:
         dist.barrier()
         return
     pairs = float(args.jobs) * args.nodes
     achieved = (score_b / 1e9) / (score_ms / 1e3) if score_ms > 0 else 0.0
     traffic, traffic_src = None, None
-    pmc = os.path.join(REPO, "profiles", "r01_pmc.json")
-    if os.path.exists(pmc):  # HBM-side bytes per launch from rocprofv3 PMC passes
-        with open(pmc) as f:
-            k = [v for n, v in json.load(f)["kernels"].items() if n.startswith("k_score")]
-        if k:
-            traffic = k[0]["traffic_bytes_per_launch"]
-            traffic_src = "profiles/r01_pmc.json (FETCH_SIZE x2 + WRITE_SIZE, tools/gpu_evidence.sh)"
+    for pmc in ("r02_pmc.json", "r01_pmc.json"):  # HBM-side bytes per launch (rocprofv3 PMC)
+        path = os.path.join(REPO, "profiles", pmc)
+        if os.path.exists(path):
+            with open(path) as f:
+                k = [v for n, v in json.load(f)["kernels"].items() if n.startswith("k_score")]
+            if k:
+                traffic = k[0]["traffic_bytes_per_launch"]
+                traffic_src = f"profiles/{pmc} (FETCH_SIZE x2 + WRITE_SIZE, tools/gpu_evidence.sh)"
+            break
     out = {
         "metric": METRIC,
         "value": pairs / (ms / 1e3),
         "unit": "pairs/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms,
@@ -195,9 +333,13 @@ def main():
                    "jobs": args.jobs, "nodes": args.nodes, "dims": 4,
                    "units": st["units"], "rounds": st["rounds"], "passes": st["passes"],
                    "placed_jobs": st["placed"], "pairs_scored": st["pairs"],
-                   "parallelism": f"job-row shards x{world}"},
-        "latency_ms": ms,
-        "roofline": {"bound": "hbm", "kernel": "k_score (filter+score, materialised matrix)",
+                   "parallelism": parallelism},
+        "solve_ms": ms,
+        "latency_ms": latency_ms,
+        "latency_def": "kp_place host->host (validate, H2D, solve, D2H), median of "
+                       f"{len(lat)}",
+        "pairs_scored_per_s": st["pairs"] / (ms / 1e3),
+        "roofline": {"bound": "hbm", "kernel": "k_score32 (filter+score, materialised matrix)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
@@ -206,10 +348,12 @@ def main():
                      "launches_per_step": launches / args.steps,
                      "avg_launch_ms": score_ms / max(launches, 1)},
     }
-    if not args.no_cpu_baseline and world == 1:
-        out["cpu_baseline"] = cpu_baseline(args)
-    if not args.no_stream and world == 1:
-        out["streaming"] = streaming(args)
+    if not args.no_config4 and n_gpus == 1:
+        out["config4"] = config4(args, make_placer)
+    if not args.no_stream and n_gpus == 1:
+        out["streaming"] = streaming(args, make_placer)
+    if not args.no_cpu_baseline and n_gpus == 1:
+        out["cpu_baseline"] = cpu_baseline(args, w, p)
     line = json.dumps(out)
     print(line, flush=True)
     if args.out:

@@ -150,11 +150,12 @@ static int ensure_units(kp_ctx *c, int32_t U, int32_t J) {
     KP_TRY(dalloc(&c->d.s0, pm));
     KP_TRY(dalloc(&c->d.bid, pm));
     KP_TRY(dalloc(&c->d.gpart, pm));
+    KP_TRY(dalloc(&c->d.win, pm / 64 + 128));
+    KP_TRY(dalloc(&c->d.winmin, (pm / 64 + 128) * KP_MAX_DIMS));
     KP_TRY(dalloc(&c->d.nparts, u));
     KP_TRY(dalloc(&c->d.arrive, u));
     KP_TRY(dalloc(&c->d.uprio, u));
     KP_TRY(dalloc(&c->d.plist, u));
-    KP_TRY(dalloc(&c->d.win, pm / 64 + 128));
     KP_TRY(dalloc(&c->d.inv, pm));
     KP_TRY(dalloc(&c->d.ent_unit, pm));
     KP_TRY(dalloc(&c->d.ent_slot, pm));
@@ -547,6 +548,18 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
                             c->stream));
     KP_HIP(hipStreamSynchronize(c->stream));
   }
+  {  // every buffer the solve's kernels touch exists (never launch on a null)
+    const DevState &d = c->d;
+    const void *need[] = {d.cap, d.used, d.R32, d.K32, d.base, d.topo, d.np32, d.q, d.leader,
+                          d.size, d.status, d.salt, d.aff, d.job_node, d.job_score, d.job_status,
+                          d.act, d.act_local, d.cand, d.cand_local, d.open, d.flag, d.s0, d.bid,
+                          d.win, d.winmin, d.gpart, d.nparts, d.arrive, d.inv, d.ent_unit,
+                          d.ent_slot, d.ent_size, d.ent_lead, d.ent_q, d.csr_kin, d.csr_vin,
+                          d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.node_flag, d.node_list,
+                          d.pass_flag, d.counters, d.stats, d.temp};
+    for (const void *ptr : need)
+      if (!ptr) return fail(KP_ENOMEM, "kp_solve: a device buffer is missing");
+  }
   KP_TRY(launch_reset_units(c));
   const int64_t rpc = rows_per_chunk(c);
   const int32_t shard = c->u_hi - c->u_lo;
@@ -840,7 +853,7 @@ void kp_destroy(kp_ctx *c) {
   void *ptrs[] = {d.cap, d.used, d.used0, d.R32, d.K32, d.base, d.topo, d.q, d.leader, d.size,
                   d.status, d.salt, d.aff,
                   d.job_node, d.job_score, d.job_status, d.act_local, d.cand_local, d.score,
-                  d.mask, d.open, d.flag, d.s0, d.bid, d.gpart, d.nparts, d.arrive, d.win,
+                  d.mask, d.open, d.flag, d.s0, d.bid, d.gpart, d.nparts, d.arrive, d.win, d.winmin,
                   d.inv, d.ent_unit,
                   d.ent_slot, d.ent_size, d.ent_lead, d.ent_q,
                   d.csr_kin, d.csr_vin,

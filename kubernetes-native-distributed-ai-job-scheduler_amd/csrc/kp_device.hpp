@@ -68,6 +68,45 @@ __device__ __forceinline__ int64_t wave_incl_scan_i64(int64_t v) {
   if (l >= 32) v += t;
   return v;
 }
+// 32-bit inclusive prefix sum over the 64 lanes (same DPP pattern)
+__device__ __forceinline__ int32_t wave_incl_scan_i32(int32_t v) {
+  const int l = lane_id(), rl = l & 15;
+  int32_t t;
+  t = __builtin_amdgcn_mov_dpp(v, 0x111, 0xf, 0xf, false);
+  if (rl >= 1) v += t;
+  t = __builtin_amdgcn_mov_dpp(v, 0x112, 0xf, 0xf, false);
+  if (rl >= 2) v += t;
+  t = __builtin_amdgcn_mov_dpp(v, 0x114, 0xf, 0xf, false);
+  if (rl >= 4) v += t;
+  t = __builtin_amdgcn_mov_dpp(v, 0x118, 0xf, 0xf, false);
+  if (rl >= 8) v += t;
+  t = __builtin_amdgcn_mov_dpp(v, 0x142, 0xf, 0xf, false);  // row_bcast:15
+  if ((l & 31) >= 16) v += t;
+  t = __builtin_amdgcn_mov_dpp(v, 0x143, 0xf, 0xf, false);  // row_bcast:31
+  if (l >= 32) v += t;
+  return v;
+}
+
+// position of the r-th set bit (r < popcount(x)) of x: popcount bisection
+__device__ __forceinline__ int select_bit(uint32_t x, int r) {
+  int pos = 0;
+#pragma unroll
+  for (int h = 16; h >= 1; h >>= 1) {
+    const int c = __popc(x & ((1u << h) - 1u));
+    if (r >= c) {
+      r -= c;
+      x >>= h;
+      pos += h;
+    }
+  }
+  return pos;
+}
+
+__device__ __forceinline__ int select_bit64(uint64_t x, int r) {
+  const int lo = __popc((uint32_t)x);
+  return r < lo ? select_bit((uint32_t)x, r) : 32 + select_bit((uint32_t)(x >> 32), r - lo);
+}
+
 // max over aligned groups of G lanes (G = 16, 32 or 64), result in every
 // lane of the group: DPP max-scan inside the group, then the group's last
 // lane is read back with scalar readlanes (no LDS crossbar)

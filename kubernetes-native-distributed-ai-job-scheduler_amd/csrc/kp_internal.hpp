@@ -78,7 +78,8 @@ struct DevState {
   // count and an arrival counter (the last accepted part commits the gang)
   int32_t *s0 = nullptr;        // [U*K]
   uint32_t *bid = nullptr;      // [U*K] (pass << 8) | members
-  int32_t *win = nullptr;       // [U*K/64 + 64]
+  int32_t *win = nullptr;       // [U*K/64 + 64] last pass with a bid in each 64-entry window
+  int64_t *winmin = nullptr;    // [D][P/64 + 64] smallest request per 64-entry window
   int4 *gpart = nullptr;        // [U*K]
   int32_t *nparts = nullptr;    // [U]
   int32_t *arrive = nullptr;    // [U]

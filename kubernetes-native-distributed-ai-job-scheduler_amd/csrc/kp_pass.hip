@@ -86,11 +86,27 @@ __global__ void k_csr_finish(int32_t P, int32_t N, int32_t K, int32_t D, int32_t
                              int32_t *__restrict__ inv, int32_t *__restrict__ ent_unit,
                              int32_t *__restrict__ ent_slot, int32_t *__restrict__ ent_size,
                              int32_t *__restrict__ ent_lead, int64_t *__restrict__ ent_q,
-                             int32_t *__restrict__ node_list, int32_t *__restrict__ nl_count) {
-  int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= P) return;
-  const uint32_t k = keys[e];
-  if (k >= (uint32_t)N) return;
+                             int32_t *__restrict__ node_list, int32_t *__restrict__ nl_count,
+                             int64_t *__restrict__ winmin, int64_t nwin) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t k = e < P ? keys[e] : (uint32_t)N;
+  // per 64-entry window (= this wave's entries) the smallest request per dim:
+  // a lower bound on every bid in it (a bid is members x request), which
+  // lets accept skip windows no bidder of which fits any more
+  {
+    const int32_t u = k < (uint32_t)N ? act[(int32_t)(vals[e] >> 5)] : 0;
+    const int w = e >> 6;
+    for (int d = 0; d < D; ++d) {
+      uint64_t x = k < (uint32_t)N ? (uint64_t)q[(int64_t)d * U + u] : ~0ull;
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) {
+        const uint64_t o = shfl_xor_u64(x, m);
+        x = o < x ? o : x;
+      }
+      if ((threadIdx.x & 63) == 0 && w < nwin) winmin[(int64_t)d * nwin + w] = (int64_t)x;
+    }
+  }
+  if (e >= P || k >= (uint32_t)N) return;
   const uint32_t v = vals[e];
   const int32_t a = (int32_t)(v >> 5), c = (int32_t)(v & 31u);
   const int32_t u = act[a];
@@ -153,7 +169,11 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
   const int32_t u0 = pa.act[aa];
   const int32_t node = gl < K ? pa.cand[(int64_t)aa * K + gl] : -1;
   const int32_t e_inv = gl < K ? pa.inv[(int64_t)aa * K + gl] : 0;  // valid iff node >= 0
+  const int32_t prev = pass > 0 ? pa.pass_flag[pass - 1] : 1;
   const int32_t A = pa.A_dev ? min(pa.A, *pa.A_dev) : pa.A;
+  // a pass after one without proposals has none either (usage unchanged,
+  // open slots only close): the round is over
+  if (!prev) return;
   const bool in = a < A;
   const bool slot_ok = in && op;
   if (__ballot(slot_ok) == 0) return;
@@ -431,11 +451,16 @@ struct AccArgs {
   const int64_t *ent_q;
   const int32_t *ent_unit, *ent_size, *ent_lead, *ent_slot;
   const int64_t *cap;
-  const int32_t *node_flag, *node_list, *nl_count;
+  const int32_t *node_flag, *node_list, *nl_count, *pass_flag;
+  const int64_t *winmin;
+  int64_t nwin;
   AcceptOut o;
 };
 
-// the bidders of `node` in pass `pass` (whole wave)
+// the bidders of `node` in pass `pass` (whole wave). Flagged windows whose
+// smallest request no longer fits the node's remaining capacity in some dim
+// are skipped unread (a contested node fills after a few windows; the rest of
+// its long bidder row is then rejected without loading it).
 template <int D>
 __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int node) {
   const int lane = threadIdx.x & 63;
@@ -455,8 +480,18 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
   constexpr int BATCH = 4;  // flagged windows whose operands are loaded together
   for (int wb = w0; wb <= w1; wb += 64) {
     // a one-window segment is loaded without consulting its window flag
-    uint64_t flagged = w0 == w1 ? 1ull : __ballot(wb + lane <= w1 && ac.win[wb + lane] == pass);
-    while (flagged) {
+    const int wi = wb + lane;
+    const bool mine = wi <= w1;
+    int64_t wmin[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) wmin[d] = mine ? ac.winmin[(int64_t)d * ac.nwin + wi] : 0;
+    uint64_t flagged = w0 == w1 ? 1ull : __ballot(mine && ac.win[wi] == pass);
+    while (true) {
+      bool can = true;
+#pragma unroll
+      for (int d = 0; d < D; ++d) can &= wmin[d] <= rem[d];
+      flagged &= __ballot(can);
+      if (!flagged) break;
       int wl[BATCH];
 #pragma unroll
       for (int t = 0; t < BATCH; ++t) {
@@ -486,16 +521,17 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
 }
 
 // One wave per node: the nodes with bidders this round (use_list, small
-// rounds) or every node.
+// rounds) or every node; nothing to do after a pass without proposals.
 template <int D>
 __global__ __launch_bounds__(256) void k_accept(AccArgs ac, int32_t pass, int32_t use_list) {
   const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int32_t pf = ac.pass_flag[pass];
   int node = wv;
-  if (use_list) {  // list entry and count loaded together (wv < P < N: in bounds)
+  if (use_list) {  // list entry and count loaded together (node_list has 4 spare entries)
     const int32_t nd = ac.node_list[wv];
-    if (wv >= *ac.nl_count) return;
+    if (wv >= *ac.nl_count || !pf) return;
     node = nd;
-  } else if (node >= ac.sp.N) {
+  } else if (node >= ac.sp.N || !pf) {
     return;
   }
   accept_node<D>(ac, pass, node);
@@ -552,6 +588,9 @@ static AccArgs acc_args(kp_ctx *c, const ScoreParams &sp, int64_t P) {
   ac.node_flag = c->d.node_flag;
   ac.node_list = c->d.node_list;
   ac.nl_count = c->d.counters + 32;
+  ac.pass_flag = c->d.pass_flag;
+  ac.winmin = c->d.winmin;
+  ac.nwin = (P + 63) / 64 + 64;
   AcceptOut &o = ac.o;
   o.N = c->N;
   o.U = c->U;
@@ -653,7 +692,7 @@ int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev) {
                      c->N, K, c->D, c->U, c->d.csr_keys, c->d.csr_vals, c->d.act, c->d.q,
                      c->d.size, c->d.leader, c->d.seg_start, c->d.seg_end, c->d.inv,
                      c->d.ent_unit, c->d.ent_slot, c->d.ent_size, c->d.ent_lead, c->d.ent_q,
-                     c->d.node_list, c->d.counters + 32);
+                     c->d.node_list, c->d.counters + 32, c->d.winmin, nwin);
   KP_HIP(hipGetLastError());
   return KP_OK;
 }

@@ -14,6 +14,8 @@ from __future__ import annotations
 import copy
 import datetime as _dt
 
+import numpy as np
+
 from . import _abi
 
 COND_TYPE = "Placed"
@@ -24,28 +26,47 @@ def _now() -> str:
 
 
 def conditions(packed, result: dict, preemption: dict | None = None, now: str | None = None):
-    """{(namespace, name): condition dict} for every CR of the packed batch."""
+    """{(namespace, name): condition dict} for every CR of the packed batch,
+    plus a Placed=False / Invalid condition for every CR the packer rejected.
+    Jobs are grouped by CR once (their rows are contiguous per CR), so the
+    writer is O(J + CRs), not O(J x CRs)."""
     now = now or _now()
-    node, status = result["node"], result["status"]
+    node = np.asarray(result["node"])
+    status = np.asarray(result["status"])
+    n_cr = len(packed.cr_keys)
+    job_cr = np.asarray(packed.job_cr)
+    counts = np.bincount(job_cr, minlength=n_cr) if job_cr.size else np.zeros(n_cr, np.int64)
+    order = np.argsort(job_cr, kind="stable")
+    starts = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
+    ok = node[order] >= 0
+    # per CR: every replica placed (empty CRs: not placed)
+    all_ok = np.zeros(n_cr, bool)
+    nz = counts > 0
+    if ok.size:
+        all_ok[nz] = np.logical_and.reduceat(ok, starts[nz])
+    names = packed.node_names
     out = {}
     for i, key in enumerate(packed.cr_keys):
-        jobs = [j for j in range(len(packed.job_cr)) if packed.job_cr[j] == i]
-        if jobs and all(node[j] >= 0 for j in jobs):
-            msg = ", ".join(f"replica {int(packed.job_replica[j])} -> {packed.node_names[node[j]]}"
+        jobs = order[starts[i]:starts[i] + counts[i]]
+        if all_ok[i]:
+            msg = ", ".join(f"replica {int(packed.job_replica[j])} -> {names[node[j]]}"
                             for j in jobs)
             out[key] = {"type": COND_TYPE, "status": "True", "reason": "BatchPlaced",
                         "message": msg, "lastUpdateTime": now}
             continue
-        st = int(status[jobs[0]]) if jobs else _abi.KP_JOB_NO_FIT
+        st = int(status[jobs[0]]) if jobs.size else _abi.KP_JOB_NO_FIT
         reason = "RoundLimit" if st == _abi.KP_JOB_ROUND_LIMIT else "NoFit"
-        msg = f"{len(jobs)} replica(s) unplaced"
-        if preemption is not None and jobs and preemption["node"][jobs[0]] >= 0:
+        msg = f"{jobs.size} replica(s) unplaced"
+        if preemption is not None and jobs.size and preemption["node"][jobs[0]] >= 0:
             j = jobs[0]
-            msg += (f"; nominated {packed.node_names[preemption['node'][j]]} "
+            msg += (f"; nominated {names[preemption['node'][j]]} "
                     f"(evicts {int(preemption['victims'][j])}, priority cost "
                     f"{int(preemption['cost'][j])})")
         out[key] = {"type": COND_TYPE, "status": "False", "reason": reason, "message": msg,
                     "lastUpdateTime": now}
+    for key, why in getattr(packed, "invalid", {}).items():
+        out[key] = {"type": COND_TYPE, "status": "False", "reason": "Invalid",
+                    "message": why, "lastUpdateTime": now}
     return out
 
 

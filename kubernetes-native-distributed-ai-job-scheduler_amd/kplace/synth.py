@@ -240,6 +240,43 @@ def config1_objects(sample_specs: list[dict], K: int = 100, N: int = 64):
     return crs, nodes
 
 
+def workload_objects(w: Workload, shared_every: int = 0):
+    """A workload as API objects for the host path (packer -> kp_place ->
+    binder): one LLMService CR per gang (replicas = gang size, gpuPerReplica
+    and gpuMemory from the job's request, priority annotation) and one Node
+    per node (allocatable cpu / memory / amd.com/gpu, per-GPU memory label,
+    xGMI island label = topo domain). The CRD has no cpu/mem fields, so the
+    packed queue carries gpu and gpu memory only. Every `shared_every`-th CR
+    uses CacheStrategy shared with a coordinator pod on node (CR index mod
+    N); returns (crs, nodes, pod_nodes)."""
+    J, N = w.J, w.N
+    starts = np.flatnonzero(np.r_[True, (w.gang_id[1:] != w.gang_id[:-1]) | (w.gang_id[1:] < 0)])
+    sizes = np.diff(np.r_[starts, J])
+    crs, pod_nodes = [], {}
+    for i, (j, sz) in enumerate(zip(starts.tolist(), sizes.tolist())):
+        spec = {"model": f"org/model-{i % 13}", "replicas": int(sz),
+                "gpuPerReplica": int(w.req[2, j]), "gpuMemory": f"{int(w.req[3, j])}Mi"}
+        cr = {"metadata": {"name": f"llm-{i}", "namespace": "default",
+                           "annotations": {"kubeinfer.ai/priority": str(int(w.prio[j]))}},
+              "spec": spec}
+        if shared_every and i % shared_every == 0:
+            spec["cacheStrategy"] = "shared"
+            cr["status"] = {"cacheCoordinator": f"llm-{i}-coord"}
+            pod_nodes[("default", f"llm-{i}-coord")] = f"node-{i % N:05d}"
+        crs.append(cr)
+    nodes = []
+    for n in range(N):
+        g = int(w.cap[2, n])
+        labels = {"kubeinfer.ai/xgmi-island": f"island-{int(w.topo[n]):05d}"}
+        if g:
+            labels["kubeinfer.ai/gpu-memory"] = f"{int(w.cap[3, n]) // g}Mi"
+        nodes.append({"metadata": {"name": f"node-{n:05d}", "labels": labels},
+                      "status": {"allocatable": {"cpu": f"{int(w.cap[0, n])}m",
+                                                 "memory": f"{int(w.cap[1, n])}Mi",
+                                                 "amd.com/gpu": str(g)}}})
+    return crs, nodes, pod_nodes
+
+
 # scoring knobs per config (DESIGN.md §2.7)
 CONFIG_PARAMS = {
     2: dict(w_dim=(1, 1, 1, 1), w_gpu_fit=0, w_spread=0),

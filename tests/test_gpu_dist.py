@@ -76,9 +76,21 @@ def test_sharded_gpu_solve_matches_oracle(oracle, world, cfg, mpm):
     procs = [ctx.Process(target=_worker, args=(r, world, port, cfg, mpm, q)) for r in range(world)]
     for pr in procs:
         pr.start()
-    res = q.get(timeout=240)
+    import queue
+    res = None
+    for _ in range(240):  # fail fast when a worker dies instead of waiting out the timeout
+        try:
+            res = q.get(timeout=1)
+            break
+        except queue.Empty:
+            if any(pr.exitcode not in (None, 0) for pr in procs):
+                break
     for pr in procs:
         pr.join(timeout=60)
+        if pr.is_alive():
+            pr.kill()
+    assert res is not None, f"a rank failed: exit codes {[pr.exitcode for pr in procs]}"
+    for pr in procs:
         assert pr.exitcode == 0
     ok, r1, r0, p1, p0 = res
     assert ok, "sharded GPU placement differs from the oracle"

@@ -127,3 +127,119 @@ def test_status_writer_replaces_only_its_condition():
     assert st["availableReplicas"] == 2
     assert [c["type"] for c in st["conditions"]] == ["Ready", "Placed"]
     assert st["conditions"][1]["status"] == "True"
+
+
+# ---------------------------------------------------------------------------
+# invalid objects, failing batches, CacheStrategy shared, scale
+# ---------------------------------------------------------------------------
+def _nodes(n=4):
+    return [{"metadata": {"name": f"n{i}", "labels": {"kubeinfer.ai/gpu-memory": "288Gi",
+                                                      "kubeinfer.ai/xgmi-island": f"isl-{i // 2}"}},
+             "status": {"allocatable": {"cpu": "128", "memory": "1Ti", "amd.com/gpu": "8"}}}
+            for i in range(n)]
+
+
+def test_bad_cr_and_bad_node_do_not_abort_the_batch(oracle):
+    crs = [{"metadata": {"name": "good-a"}, "spec": {"model": "m", "replicas": 2, "gpuPerReplica": 1}},
+           {"metadata": {"name": "too-big"}, "spec": {"model": "m", "replicas": 65}},
+           {"metadata": {"name": "bad-mem"}, "spec": {"model": "m", "gpuMemory": "24G"}},
+           {"metadata": {"name": "good-b"}, "spec": {"model": "m", "gpuPerReplica": 2}}]
+    nodes = _nodes() + [{"metadata": {"name": "broken"},
+                         "status": {"allocatable": {"cpu": "lots"}}}]
+    written = {}
+    r = runner.BatchRunner(OraclePlacer(oracle), lambda: crs, lambda: nodes,
+                           lambda k, st: written.__setitem__(k, st), _abi.default_params())
+    s = r.run_batch()
+    assert s["invalid_crs"] == 2 and s["bad_nodes"] == 1 and s["nodes"] == 5
+    cond = {k[1]: v["conditions"][0] for k, v in written.items()}
+    assert cond["good-a"]["status"] == "True" and cond["good-b"]["status"] == "True"
+    assert cond["too-big"]["reason"] == "Invalid" and "gang limit" in cond["too-big"]["message"]
+    assert cond["bad-mem"]["reason"] == "Invalid"
+    assert "broken" not in cond["good-a"]["message"]
+
+
+def test_serve_survives_a_failing_batch(oracle):
+    import threading
+
+    class Flaky(OraclePlacer):
+        calls = 0
+
+        def place(self, w, p):
+            Flaky.calls += 1
+            if Flaky.calls == 1:
+                raise RuntimeError("transient engine failure")
+            return super().place(w, p)
+
+    crs = [{"metadata": {"name": "a"}, "spec": {"model": "m"}}]
+    written = {}
+    r = runner.BatchRunner(Flaky(oracle), lambda: crs, lambda: _nodes(),
+                           lambda k, st: written.__setitem__(k, st), _abi.default_params(),
+                           debounce_s=0.0, retry_s=0.01)
+    stop = threading.Event()
+    t = threading.Thread(target=r.serve, args=(stop, 0.01))
+    t.start()
+    r.reconcile(("default", "a"))
+    for _ in range(500):
+        if written:
+            break
+        stop.wait(0.01)
+    stop.set()
+    t.join(5)
+    assert Flaky.calls >= 2 and written[("default", "a")]["conditions"][0]["status"] == "True"
+
+
+def test_cache_shared_affinity_packing():
+    cache = [c for c in samples() if c["spec_in"].get("cacheStrategy") == "shared"][0]
+    crs = [{"metadata": {"name": "test-cache-llm", "namespace": "default"},
+            "spec": cache["spec_in"], "status": {"cacheCoordinator": "test-cache-llm-0"}},
+           {"metadata": {"name": "same-model", "namespace": "default"},
+            "spec": dict(cache["spec_in"], replicas=1)},                   # no coordinator yet
+           {"metadata": {"name": "plain", "namespace": "default"},
+            "spec": {"model": cache["spec_in"]["model"]}}]                 # cacheStrategy none
+    pk = packer.pack(crs, _nodes(), pod_nodes={("default", "test-cache-llm-0"): "n3"})
+    w = pk.workload
+    dom = int(w.topo[pk.node_names.index("n3")])
+    assert w.affinity.tolist() == [dom] * 3 + [dom] + [-1]
+    # without the pod map the coordinator's domain is unknown
+    assert (packer.pack(crs, _nodes()).workload.affinity == -1).all()
+
+
+def test_cache_shared_sample_places_in_coordinator_domain(oracle):
+    cache = [c for c in samples() if c["spec_in"].get("cacheStrategy") == "shared"][0]
+    crs = [{"metadata": {"name": "test-cache-llm", "namespace": "default"},
+            "spec": cache["spec_in"], "status": {"cacheCoordinator": "coord"}}]
+    pk = packer.pack(crs, _nodes(8), pod_nodes={("default", "coord"): "n5"})
+    res = OraclePlacer(oracle).place(pk.workload, _abi.default_params(**synth.CONFIG_PARAMS[1]))
+    doms = {int(pk.workload.topo[n]) for n in res["node"]}
+    assert doms == {int(pk.workload.topo[5])}
+
+
+def _naive_conditions(packed, result):
+    out = {}
+    for i, key in enumerate(packed.cr_keys):
+        jobs = [j for j in range(len(packed.job_cr)) if packed.job_cr[j] == i]
+        out[key] = bool(jobs) and all(result["node"][j] >= 0 for j in jobs)
+    return out
+
+
+def test_binder_grouping_matches_naive_and_scales():
+    import time
+    w = synth.config3(3_000, 200)
+    crs, nodes, pods = synth.workload_objects(w, shared_every=7)
+    pk = packer.pack(crs, nodes, pod_nodes=pods)
+    rng = np.random.default_rng(0)
+    res = {"node": np.where(rng.random(pk.workload.J) < 0.7,
+                            rng.integers(0, pk.workload.N, pk.workload.J), -1).astype(np.int32),
+           "status": np.zeros(pk.workload.J, np.int32)}
+    got = binder.conditions(pk, res, now="t")
+    naive = _naive_conditions(pk, res)
+    assert {k: v["status"] == "True" for k, v in got.items()} == naive
+    # config #3 scale: 26k CRs / 100k jobs in well under a second of grouping
+    w = synth.config3()
+    crs, nodes, _ = synth.workload_objects(w)
+    t = time.perf_counter()
+    pk = packer.pack(crs, nodes)
+    res = {"node": np.zeros(pk.workload.J, np.int32), "status": np.zeros(pk.workload.J, np.int32)}
+    conds = binder.conditions(pk, res, now="t")
+    assert len(conds) == len(crs) == 26_525
+    assert time.perf_counter() - t < 30
