@@ -224,6 +224,105 @@ struct Vec<4> {
   }
 };
 
+// The row loop of k_score32 for one wave's tile (registers of its NPL nodes
+// per lane). FAST: no node of the wave needs the W form of the division, so
+// every dim runs the branch-free 24-bit form (E-mode nodes included: their
+// estimate is exact and the remainder check is a no-op); else each dim picks
+// its form (W waves: 64-bit products).
+template <int D, bool MOST, int NPL, bool FAST>
+__device__ __forceinline__ void score_rows(
+    const ScoreParams &sp, const uint32_t (&sq)[kScoreMaxRows][D + 2], int r0, int r1,
+    const uint32_t (&f_)[NPL][D], const uint32_t (&u_)[NPL][D], const uint32_t (&c_)[NPL][D],
+    const uint32_t (&R_)[NPL][D], const uint32_t (&k_)[NPL][D], const uint32_t (&fg_)[NPL],
+    const uint32_t (&tp_)[NPL], const int32_t (&b_)[NPL], const bool (&v_)[NPL],
+    const bool (&anyW)[D], const bool (&allE)[D], int32_t *__restrict__ score,
+    uint64_t *__restrict__ mask, int32_t Ns, int tile0, int nb, int lane) {
+  const int words = Ns >> 6;
+  const bool store_ok = nb < Ns;  // Ns % 64 == 0: then all NPL nodes are in the row
+  const int32_t wfit = sp.w_gpu_fit, waff = sp.w_affinity;
+  const uint32_t S = (uint32_t)sp.S;
+  for (int r = r0; r < r1; ++r) {
+    uint32_t qq[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) qq[d] = sq[r - r0][d];
+    const uint32_t qg = sq[r - r0][D], af = sq[r - r0][D + 1];
+    bool fits[NPL];
+    int32_t acc[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      fits[k] = v_[k];
+      acc[k] = 0;
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) {
+        fits[k] &= qq[d] <= f_[k][d];
+        // infeasible pairs may compute garbage (operands past 24 bits,
+        // wrapped sums): masked below
+        const uint32_t x = u_[k][d] + qq[d];
+        uint32_t util;
+        if (!FAST && anyW[d]) {
+          bool nz;
+          const uint32_t t = div_floor32(x, c_[k][d], R_[k][d], k_[k][d], S, nz);
+          util = MOST ? t : t + (nz ? 1u : 0u);
+        } else {
+          uint32_t t = mul_u24(x, R_[k][d]) >> k_[k][d];
+          if (!FAST && MOST && allE[d]) {
+            util = t;
+          } else {
+            // r = x*S - t*c lies in [0, 2c) and c < 2^24: exact mod 2^32
+            uint32_t rr = mul_u24(x, S) - mul_u24(t, c_[k][d]);
+            const bool up = rr >= c_[k][d];
+            t += up ? 1u : 0u;
+            if (MOST) {
+              util = t;
+            } else {
+              rr -= up ? c_[k][d] : 0u;
+              util = t + (rr != 0u ? 1u : 0u);
+            }
+          }
+        }
+        acc[k] += (int32_t)__umul24((uint32_t)sp.w[d], util);
+      }
+    }
+    int32_t sv[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      // GPU-topology fit: the job takes exactly the node's free GPUs;
+      // CacheStrategy shared: the node is in the job's affinity domain
+      const int32_t bonus = ((qg != 0u && fg_[k] == qg) ? wfit : 0) + (tp_[k] == af ? waff : 0);
+      const int32_t s = (MOST ? acc[k] : b_[k] - acc[k]) + bonus;
+      sv[k] = fits[k] ? s : KP_SCORE_INFEASIBLE;
+    }
+    if (score && store_ok) {
+      if constexpr (NPL == 4)
+        *reinterpret_cast<int4 *>(score + (int64_t)r * Ns + nb) =
+            make_int4(sv[0], sv[1], sv[2], sv[3]);
+      else
+        *reinterpret_cast<int2 *>(score + (int64_t)r * Ns + nb) = make_int2(sv[0], sv[1]);
+    }
+    if (mask) {  // wave-uniform: the solve passes no mask (the -1 sentinel is the filter)
+      uint64_t bal[NPL];
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) bal[k] = __ballot(fits[k]);
+      // word i of the wave's tile: bit NPL*j + k = ballot_k bit (64/NPL)*i + j
+      if (lane < NPL && tile0 + 64 * lane < Ns) {
+        uint64_t wd = 0;
+        if constexpr (NPL == 4) {
+          const int sh = 16 * lane;
+          wd = spread4_16(bal[0] >> sh) | (spread4_16(bal[1] >> sh) << 1) |
+               (spread4_16(bal[2] >> sh) << 2) | (spread4_16(bal[3] >> sh) << 3);
+        } else {
+          const int sh = 32 * lane;
+          wd = spread2_32(bal[0] >> sh) | (spread2_32(bal[1] >> sh) << 1);
+        }
+        mask[(int64_t)r * words + (tile0 >> 6) + lane] = wd;
+      }
+    }
+  }
+}
+
 template <int D, bool MOST, int NPL>
 __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
                                                  const uint32_t *__restrict__ np, int32_t P,
@@ -305,88 +404,15 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
   }
   __syncthreads();
   if (tile0 >= Ns) return;  // wave-uniform, after the only barrier
-  const int words = Ns >> 6;
-  const bool store_ok = nb < Ns;  // Ns % 64 == 0: then all NPL nodes are in the row
-  const int32_t wfit = sp.w_gpu_fit, waff = sp.w_affinity;
-  const uint32_t S = (uint32_t)sp.S;
-  for (int r = r0; r < r1; ++r) {
-    uint32_t qq[D];
+  bool slow = false;
 #pragma unroll
-    for (int d = 0; d < D; ++d) qq[d] = sq[r - r0][d];
-    const uint32_t qg = sq[r - r0][D], af = sq[r - r0][D + 1];
-    bool fits[NPL];
-    int32_t acc[NPL];
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      fits[k] = v_[k];
-      acc[k] = 0;
-    }
-    // dim-outer: wave-uniform branches per dim for the division form
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      uint32_t util[NPL];
-#pragma unroll
-      for (int k = 0; k < NPL; ++k) {
-        fits[k] &= qq[d] <= f_[k][d];
-        // infeasible pairs may compute garbage (operands past 24 bits,
-        // wrapped sums): masked below
-        const uint32_t x = u_[k][d] + qq[d];
-        if (anyW[d]) {
-          bool nz;
-          const uint32_t t = div_floor32(x, c_[k][d], R_[k][d], k_[k][d], S, nz);
-          util[k] = MOST ? t : t + (nz ? 1u : 0u);
-        } else {
-          uint32_t t = mul_u24(x, R_[k][d]) >> k_[k][d];
-          if (MOST && allE[d]) {
-            util[k] = t;
-          } else {
-            // r = x*S - t*c lies in [0, 2c) and c < 2^24: exact mod 2^32
-            uint32_t rr = mul_u24(x, S) - mul_u24(t, c_[k][d]);
-            const bool up = rr >= c_[k][d];
-            t += up ? 1u : 0u;
-            rr -= up ? c_[k][d] : 0u;
-            util[k] = MOST ? t : t + (rr != 0u ? 1u : 0u);
-          }
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < NPL; ++k) acc[k] += (int32_t)__umul24((uint32_t)sp.w[d], util[k]);
-    }
-    int32_t sv[NPL];
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      // GPU-topology fit: the job takes exactly the node's free GPUs;
-      // CacheStrategy shared: the node is in the job's affinity domain
-      const int32_t bonus = ((qg != 0u && fg_[k] == qg) ? wfit : 0) + (tp_[k] == af ? waff : 0);
-      const int32_t s = (MOST ? acc[k] : b_[k] - acc[k]) + bonus;
-      sv[k] = fits[k] ? s : KP_SCORE_INFEASIBLE;
-    }
-    if (score && store_ok) {
-      if constexpr (NPL == 4)
-        *reinterpret_cast<int4 *>(score + (int64_t)r * Ns + nb) =
-            make_int4(sv[0], sv[1], sv[2], sv[3]);
-      else
-        *reinterpret_cast<int2 *>(score + (int64_t)r * Ns + nb) = make_int2(sv[0], sv[1]);
-    }
-    if (mask) {  // wave-uniform: the solve passes no mask (the -1 sentinel is the filter)
-      uint64_t bal[NPL];
-#pragma unroll
-      for (int k = 0; k < NPL; ++k) bal[k] = __ballot(fits[k]);
-      // word i of the wave's tile: bit NPL*j + k = ballot_k bit (64/NPL)*i + j
-      if (lane < NPL && tile0 + 64 * lane < Ns) {
-        uint64_t wd = 0;
-        if constexpr (NPL == 4) {
-          const int sh = 16 * lane;
-          wd = spread4_16(bal[0] >> sh) | (spread4_16(bal[1] >> sh) << 1) |
-               (spread4_16(bal[2] >> sh) << 2) | (spread4_16(bal[3] >> sh) << 3);
-        } else {
-          const int sh = 32 * lane;
-          wd = spread2_32(bal[0] >> sh) | (spread2_32(bal[1] >> sh) << 1);
-        }
-        mask[(int64_t)r * words + (tile0 >> 6) + lane] = wd;
-      }
-    }
-  }
+  for (int d = 0; d < D; ++d) slow |= anyW[d];
+  if (!slow)
+    score_rows<D, MOST, NPL, true>(sp, sq, r0, r1, f_, u_, c_, R_, k_, fg_, tp_, b_, v_, anyW,
+                                   allE, score, mask, Ns, tile0, nb, lane);
+  else
+    score_rows<D, MOST, NPL, false>(sp, sq, r0, r1, f_, u_, c_, R_, k_, fg_, tp_, b_, v_, anyW,
+                                    allE, score, mask, Ns, tile0, nb, lane);
 }
 
 // ---------------------------------------------------------------------------
