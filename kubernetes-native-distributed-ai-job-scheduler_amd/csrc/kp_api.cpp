@@ -127,7 +127,8 @@ static int ensure_nodes(kp_ctx *c, int32_t N, int32_t D) {
   KP_TRY(dalloc(&c->d.node_flag, (size_t)n));
   // +4: k_accept's list mode reads node_list[wave] for up to 3 padding waves
   KP_TRY(dalloc(&c->d.node_list, (size_t)n + 4));
-  KP_TRY(dalloc(&c->d.np32, (size_t)(4 * D + 2) * (((size_t)n + 1023) & ~(size_t)1023)));
+  KP_TRY(dalloc(&c->d.perm, (size_t)n));
+  KP_TRY(dalloc(&c->d.np32, (size_t)(5 * D + 3) * (((size_t)n + 1023) & ~(size_t)1023)));
   c->cap_N = n;
   return KP_OK;
 }
@@ -359,6 +360,18 @@ static int load_nodes_impl(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap,
     if (used) std::copy(used, used + (size_t)D * N, c->h_used.begin());
     c->h_topo.resize(N);
     for (int32_t n = 0; n < N; ++n) c->h_topo[n] = topo ? topo[n] : n;
+    // canonical order: nodes sorted by capacity vector, then
+    // index; the solve's score columns follow it, so that a wave's columns
+    // share their capacities and the per-pair division becomes a per-row one
+    c->h_perm.resize(N);
+    for (int32_t n = 0; n < N; ++n) c->h_perm[n] = n;
+    std::stable_sort(c->h_perm.begin(), c->h_perm.end(), [&](int32_t a, int32_t b) {
+      for (int d = 0; d < D; ++d) {
+        const int64_t ca = cap[(int64_t)d * N + a], cb = cap[(int64_t)d * N + b];
+        if (ca != cb) return ca < cb;
+      }
+      return false;
+    });
   } catch (const std::bad_alloc &) {
     return fail(KP_ENOMEM, "kp_load_nodes: host copy");
   }
@@ -371,6 +384,8 @@ static int load_nodes_impl(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap,
     KP_HIP(hipMemcpyAsync(c->d.used0, c->d.used, sizeof(int64_t) * D * N,
                           hipMemcpyDeviceToDevice, c->stream));
     KP_HIP(hipMemcpyAsync(c->d.topo, c->h_topo.data(), sizeof(int32_t) * N,
+                          hipMemcpyHostToDevice, c->stream));
+    KP_HIP(hipMemcpyAsync(c->d.perm, c->h_perm.data(), sizeof(int32_t) * N,
                           hipMemcpyHostToDevice, c->stream));
   }
   // the victim pool belongs to the previous node table
@@ -550,7 +565,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   }
   {  // every buffer the solve's kernels touch exists (never launch on a null)
     const DevState &d = c->d;
-    const void *need[] = {d.cap, d.used, d.R32, d.K32, d.base, d.topo, d.np32, d.q, d.leader,
+    const void *need[] = {d.cap, d.used, d.R32, d.K32, d.base, d.topo, d.perm, d.np32, d.q, d.leader,
                           d.size, d.status, d.salt, d.aff, d.job_node, d.job_score, d.job_status,
                           d.act, d.act_local, d.cand, d.cand_local, d.open, d.flag, d.s0, d.bid,
                           d.win, d.winmin, d.gpart, d.nparts, d.arrive, d.inv, d.ent_unit,
@@ -561,6 +576,8 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
       if (!ptr) return fail(KP_ENOMEM, "kp_solve: a device buffer is missing");
   }
   KP_TRY(launch_reset_units(c));
+  c->pack_sp = sp;
+  c->pack_canonical = true;  // the solve scores in canonical column order
   const int64_t rpc = rows_per_chunk(c);
   const int32_t shard = c->u_hi - c->u_lo;
   KP_TRY(ensure_matrix(c, (int32_t)std::min<int64_t>(std::max(shard, 1), rpc)));
@@ -855,7 +872,7 @@ void kp_destroy(kp_ctx *c) {
                   d.job_node, d.job_score, d.job_status, d.act_local, d.cand_local, d.score,
                   d.mask, d.open, d.flag, d.s0, d.bid, d.gpart, d.nparts, d.arrive, d.win, d.winmin,
                   d.inv, d.ent_unit,
-                  d.ent_slot, d.ent_size, d.ent_lead, d.ent_q,
+                  d.ent_slot, d.ent_size, d.ent_lead, d.ent_q, d.perm,
                   d.csr_kin, d.csr_vin,
                   d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
                   d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.roff,
@@ -1038,6 +1055,8 @@ int kp_score(kp_ctx *c, const kp_params *p, int32_t job_lo, int32_t job_hi, int3
   KP_TRY(ensure_mask(c, chunk));
   std::vector<int32_t> hs;
   std::vector<uint64_t> hm;
+  c->pack_sp = sp;
+  c->pack_canonical = false;  // kp_score returns columns in node order
   KP_TRY(launch_pack(c));  // 32-bit node planes of the current usage
   for (int64_t r0 = 0; r0 < rows; r0 += rpc) {
     const int32_t nr = (int32_t)std::min<int64_t>(rpc, rows - r0);

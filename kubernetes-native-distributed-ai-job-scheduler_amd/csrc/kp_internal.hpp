@@ -56,7 +56,8 @@ struct DevState {
   uint32_t *R32 = nullptr, *K32 = nullptr;  // [D][N] exact-division tables (div_prep)
   int64_t *base = nullptr;  // LeastAllocated base: sum of w*S over dims with cap > 0
   int32_t *topo = nullptr;
-  uint32_t *np32 = nullptr;  // [4*D+2][round_up(N,1024)] 32-bit score tile planes
+  int32_t *perm = nullptr;  // [N] canonical order: nodes sorted by (cap vector, index)
+  uint32_t *np32 = nullptr;  // [5*D+3][round_up(N,1024)] 32-bit score tile planes
   // units (rank order), job outputs
   int64_t *q = nullptr;  // [D][U]
   int32_t *leader = nullptr, *size = nullptr, *status = nullptr;
@@ -168,6 +169,11 @@ struct kp_ctx {
   // pinned host scratch
   int32_t *pinned = nullptr;  // small counters
   kp::DevState d;
+  // what the next node-plane pack builds: the solve's canonical column order
+  // (scores by perm[column]) or kp_score's node order, for these params
+  kp::ScoreParams pack_sp{};
+  bool pack_canonical = false;
+  std::vector<int32_t> h_perm;
   kp_result last{};
   kp_timing timing{};
   std::string last_error;  // detail of the last failed call (kp_last_error)

@@ -67,6 +67,7 @@ __global__ __launch_bounds__(256) void k_score(ScoreParams sp,
                                                const int64_t *__restrict__ cap,
                                                const int64_t *__restrict__ used,
                                                const int32_t *__restrict__ topo,
+                                               const int32_t *__restrict__ perm,
                                                const int64_t *__restrict__ q, int32_t qstride,
                                                const int32_t *__restrict__ uaff,
                                                const int32_t *__restrict__ rows_unit,
@@ -84,9 +85,9 @@ __global__ __launch_bounds__(256) void k_score(ScoreParams sp,
   bool v_[NPL];
 #pragma unroll
   for (int k = 0; k < NPL; ++k) {
-    const int n = tile0 + k * 64 + lane;
+    const int n = tile0 + k * 64 + lane;  // column; its node is perm[n] (canonical order)
     v_[k] = n < N;
-    const int nn = v_[k] ? n : 0;
+    const int nn = v_[k] ? (perm ? perm[n] : n) : 0;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       c_[k][d] = cap[(int64_t)d * N + nn];
@@ -151,32 +152,51 @@ __device__ __forceinline__ uint32_t mul_u24(uint32_t a, uint32_t b) {
 }
 
 
-// Round-start pack of the node table into the 32-bit form k_score32 consumes:
-// u32 SoA planes [4*d + {0: free, 1: used, 2: R, 3: K}][P] (div_prep tables),
-// the LeastAllocated base in plane 4*D and the topo domain in plane 4*D+1,
-// P = round_up(N, 1024) (whole score tiles; padding nodes are zero and masked
-// in the kernel). One 8- or 16-B load per lane and plane then fetches a
-// lane's consecutive nodes: 4*D+2 fully coalesced loads per wave instead of
-// strided gathers from the int64 table.
+// Round-start pack of the node table into the 32-bit form k_score32 consumes,
+// column i holding node perm[i] (the canonical order: nodes sorted by their
+// capacity vector; identity for kp_score). u32 SoA planes
+// [5*d + {0: free, 1: cap, 2: a, 3: R, 4: K}][P] where u*S (+ c - 1 for
+// LeastAllocated's ceiling) = A*c + a and (R, K) = div_prep(c), then the
+// LeastAllocated base, the topo domain and WA = sum_d w_d*A_d in planes 5D,
+// 5D+1, 5D+2; P = round_up(N, 1024) (whole score tiles; padding columns are
+// zero and masked). One 8- or 16-B load per lane and plane fetches a lane's
+// consecutive columns.
+constexpr int kPlanes = 5;  // u32 planes per dim
+
 template <int D>
 __device__ __forceinline__ void pack_node(const int64_t *__restrict__ cap,
                                           const int64_t *__restrict__ used,
-                                          const uint32_t *__restrict__ R32,
-                                          const uint32_t *__restrict__ K32,
                                           const int64_t *__restrict__ base,
-                                          const int32_t *__restrict__ topo, int32_t N, int32_t P,
-                                          uint32_t *__restrict__ np, int n) {
-  const bool v = n < N;
+                                          const int32_t *__restrict__ topo,
+                                          const int32_t *__restrict__ perm, int32_t N, int32_t P,
+                                          const ScoreParams &sp, uint32_t *__restrict__ np,
+                                          int i) {
+  const bool v = i < N;
+  const int n = v ? (perm ? perm[i] : i) : 0;
+  const uint64_t S = (uint64_t)sp.S;
+  uint32_t wa = 0;
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    const int64_t cc = v ? cap[(int64_t)d * N + n] : 0, uu = v ? used[(int64_t)d * N + n] : 0;
-    np[(int64_t)(4 * d + 0) * P + n] = (uint32_t)(cc - uu);
-    np[(int64_t)(4 * d + 1) * P + n] = (uint32_t)uu;
-    np[(int64_t)(4 * d + 2) * P + n] = v ? R32[(int64_t)d * N + n] : 0u;
-    np[(int64_t)(4 * d + 3) * P + n] = v ? K32[(int64_t)d * N + n] : (1u | kDivE);
+    const uint64_t cc = v ? (uint64_t)cap[(int64_t)d * N + n] : 0;
+    const uint64_t uu = v ? (uint64_t)used[(int64_t)d * N + n] : 0;
+    uint64_t A = 0, a = 0;
+    if (cc > 0) {
+      const uint64_t num = uu * S + (sp.most_allocated ? 0 : cc - 1);
+      A = num / cc;
+      a = num - A * cc;
+    }
+    uint32_t R = 0, K = 1u | kDivE;
+    div_prep(cc, (uint32_t)S, R, K);
+    wa += (uint32_t)sp.w[d] * (uint32_t)A;
+    np[(int64_t)(kPlanes * d + 0) * P + i] = (uint32_t)(cc - uu);
+    np[(int64_t)(kPlanes * d + 1) * P + i] = (uint32_t)cc;
+    np[(int64_t)(kPlanes * d + 2) * P + i] = (uint32_t)a;
+    np[(int64_t)(kPlanes * d + 3) * P + i] = R;
+    np[(int64_t)(kPlanes * d + 4) * P + i] = K;
   }
-  np[(int64_t)(4 * D) * P + n] = v ? (uint32_t)base[n] : 0u;
-  np[(int64_t)(4 * D + 1) * P + n] = v ? (uint32_t)topo[n] : 0xFFFFFFFFu;
+  np[(int64_t)(kPlanes * D) * P + i] = v ? (uint32_t)base[n] : 0u;
+  np[(int64_t)(kPlanes * D + 1) * P + i] = v ? (uint32_t)topo[n] : 0xFFFFFFFFu;
+  np[(int64_t)(kPlanes * D + 2) * P + i] = wa;
 }
 
 // Round start, one launch: active-unit flags of [lo, hi) (input of the
@@ -188,14 +208,14 @@ __global__ __launch_bounds__(256) void k_round_start(const int32_t *__restrict__
                                                      int32_t *__restrict__ flag,
                                                      const int64_t *__restrict__ cap,
                                                      const int64_t *__restrict__ used,
-                                                     const uint32_t *__restrict__ R32,
-                                                     const uint32_t *__restrict__ K32,
                                                      const int64_t *__restrict__ base,
-                                                     const int32_t *__restrict__ topo, int32_t N,
-                                                     int32_t P, uint32_t *__restrict__ np) {
+                                                     const int32_t *__restrict__ topo,
+                                                     const int32_t *__restrict__ perm, int32_t N,
+                                                     int32_t P, ScoreParams sp,
+                                                     uint32_t *__restrict__ np) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < hi - lo) flag[i] = status[lo + i] == kActive ? 1 : 0;
-  if (i < P) pack_node<D>(cap, used, R32, K32, base, topo, N, P, np, i);
+  if (i < P) pack_node<D>(cap, used, base, topo, perm, N, P, sp, np, i);
 }
 
 // bit j of a 32-bit value -> bit 2j
@@ -224,24 +244,116 @@ struct Vec<4> {
   }
 };
 
-// The row loop of k_score32 for one wave's tile (registers of its NPL nodes
-// per lane). FAST: no node of the wave needs the W form of the division, so
-// every dim runs the branch-free 24-bit form (E-mode nodes included: their
-// estimate is exact and the remainder check is a no-op); else each dim picks
-// its form (W waves: 64-bit products).
-template <int D, bool MOST, int NPL, bool FAST>
-__device__ __forceinline__ void score_rows(
-    const ScoreParams &sp, const uint32_t (&sq)[kScoreMaxRows][D + 2], int r0, int r1,
-    const uint32_t (&f_)[NPL][D], const uint32_t (&u_)[NPL][D], const uint32_t (&c_)[NPL][D],
-    const uint32_t (&R_)[NPL][D], const uint32_t (&k_)[NPL][D], const uint32_t (&fg_)[NPL],
-    const uint32_t (&tp_)[NPL], const int32_t (&b_)[NPL], const bool (&v_)[NPL],
-    const bool (&anyW)[D], const bool (&allE)[D], int32_t *__restrict__ score,
+// floor(n / c) and n mod c for a 64-bit n < 2^53 and c > 0: a double
+// estimate corrected by one step each way
+__device__ __forceinline__ void udivmod_uniform(uint64_t n, uint32_t c, uint64_t &Q, uint64_t &r) {
+  Q = (uint64_t)((double)n / (double)c);
+  int64_t rr = (int64_t)n - (int64_t)(Q * c);
+  if (rr < 0) {
+    --Q;
+    rr += c;
+  } else if (rr >= (int64_t)c) {
+    ++Q;
+    rr -= c;
+  }
+  r = (uint64_t)rr;
+}
+
+// Row loop of a wave whose columns all have the same capacity in every dim
+// (the canonical node order groups equal capacity vectors, so on a cluster
+// of a few node shapes almost every wave qualifies). With u*S = A*c + a per
+// node (pack) and q*S = Q*c + rho per row, floor((u+q)*S / c) =
+// A + Q + [a >= c - rho]: a pair costs a compare and a select per dim. The
+// weighted sums of the A's (WA) come per node from the pack, the per-row
+// thresholds c - rho and the weighted sum of the Q's (WQ) from the
+// workgroup's staging step (sx: one row of thresholds per wave, computed once
+// by one thread, not by every lane).
+constexpr uint32_t kRowNoFit = 0x80000000u;  // WQ word flag: no column of the wave fits the row
+
+template <int D, bool MOST, int NPL>
+__device__ __forceinline__ void score_rows_uniform(
+    const ScoreParams &sp, const uint32_t (&sq)[kScoreMaxRows][D + 2],
+    const uint32_t (&sx)[kScoreMaxRows][D + 1], int r0, int r1, const uint32_t (&f_)[NPL][D],
+    const uint32_t (&a_)[NPL][D], const int32_t (&wa_)[NPL], const uint32_t (&fg_)[NPL],
+    const uint32_t (&tp_)[NPL], const int32_t (&b_)[NPL], int32_t *__restrict__ score,
     uint64_t *__restrict__ mask, int32_t Ns, int tile0, int nb, int lane) {
   const int words = Ns >> 6;
-  const bool store_ok = nb < Ns;  // Ns % 64 == 0: then all NPL nodes are in the row
+  const bool store_ok = nb < Ns;
+  const int32_t wfit = sp.w_gpu_fit, waff = sp.w_affinity;
+  for (int r = r0; r < r1; ++r) {
+    uint32_t qq[D], thr[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      qq[d] = sq[r - r0][d];
+      thr[d] = sx[r - r0][d];
+    }
+    const uint32_t qg = sq[r - r0][D], af = sq[r - r0][D + 1];
+    const uint32_t wqw = sx[r - r0][D];
+    const bool row_ok = !(wqw & kRowNoFit);
+    const int32_t wq = (int32_t)(wqw & ~kRowNoFit);
+    int32_t sv[NPL];
+    bool fits[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      bool ft = row_ok;
+      int32_t acc = wa_[k] + wq;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        ft &= qq[d] <= f_[k][d];
+        acc += a_[k][d] >= thr[d] ? sp.w[d] : 0;
+      }
+      // GPU-topology fit: the job takes exactly the node's free GPUs;
+      // CacheStrategy shared: the node is in the job's affinity domain
+      const int32_t bonus = ((qg != 0u && fg_[k] == qg) ? wfit : 0) + (tp_[k] == af ? waff : 0);
+      const int32_t sc = (MOST ? acc : b_[k] - acc) + bonus;
+      fits[k] = ft;
+      sv[k] = ft ? sc : KP_SCORE_INFEASIBLE;
+    }
+    if (score && store_ok) {
+      if constexpr (NPL == 4)
+        *reinterpret_cast<int4 *>(score + (int64_t)r * Ns + nb) =
+            make_int4(sv[0], sv[1], sv[2], sv[3]);
+      else
+        *reinterpret_cast<int2 *>(score + (int64_t)r * Ns + nb) = make_int2(sv[0], sv[1]);
+    }
+    if (mask) {
+      uint64_t bal[NPL];
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) bal[k] = __ballot(fits[k]);
+      if (lane < NPL && tile0 + 64 * lane < Ns) {
+        uint64_t wd = 0;
+        if constexpr (NPL == 4) {
+          const int sh = 16 * lane;
+          wd = spread4_16(bal[0] >> sh) | (spread4_16(bal[1] >> sh) << 1) |
+               (spread4_16(bal[2] >> sh) << 2) | (spread4_16(bal[3] >> sh) << 3);
+        } else {
+          const int sh = 32 * lane;
+          wd = spread2_32(bal[0] >> sh) | (spread2_32(bal[1] >> sh) << 1);
+        }
+        mask[(int64_t)r * words + (tile0 >> 6) + lane] = wd;
+      }
+    }
+  }
+}
+
+// The row loop of k_score32 for a wave with mixed capacities: per row the
+// nodes' (c, R, K) planes are re-read (after a compiler memory barrier, so
+// they are not hoisted into registers), and each dim takes the full-rate
+// 24-bit form or, if a node of the wave needs it, the 64-bit form.
+template <int D, bool MOST, int NPL>
+__device__ __forceinline__ void score_rows_mixed(
+    const ScoreParams &sp, const uint32_t (&sq)[kScoreMaxRows][D + 2], int r0, int r1,
+    const typename Vec<NPL>::T *__restrict__ pv, int64_t PV, int64_t iv,
+    const uint32_t (&f_)[NPL][D], const uint32_t (&fg_)[NPL], const uint32_t (&tp_)[NPL],
+    const int32_t (&b_)[NPL], const bool (&v_)[NPL], int32_t *__restrict__ score,
+    uint64_t *__restrict__ mask, int32_t Ns, int tile0, int nb, int lane) {
+  using V = Vec<NPL>;
+  const int words = Ns >> 6;
+  const bool store_ok = nb < Ns;
   const int32_t wfit = sp.w_gpu_fit, waff = sp.w_affinity;
   const uint32_t S = (uint32_t)sp.S;
   for (int r = r0; r < r1; ++r) {
+    asm volatile("" ::: "memory");
     uint32_t qq[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) qq[d] = sq[r - r0][d];
@@ -255,32 +367,38 @@ __device__ __forceinline__ void score_rows(
     }
 #pragma unroll
     for (int d = 0; d < D; ++d) {
+      const typename V::T pc = pv[(kPlanes * d + 1) * PV + iv], pr = pv[(kPlanes * d + 3) * PV + iv],
+                          pk = pv[(kPlanes * d + 4) * PV + iv];
+      uint32_t wide = 0, nonE = 0;
 #pragma unroll
       for (int k = 0; k < NPL; ++k) {
+        wide |= V::at(pk, k) & kDivW;
+        nonE |= (V::at(pk, k) & kDivE) ^ kDivE;
+      }
+      const bool anyW = __ballot(wide != 0) != 0, allE = __ballot(nonE != 0) == 0;
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) {
+        const uint32_t c = V::at(pc, k), cc = c ? c : 1u, R = V::at(pr, k), kk = V::at(pk, k) & 63u;
         fits[k] &= qq[d] <= f_[k][d];
         // infeasible pairs may compute garbage (operands past 24 bits,
         // wrapped sums): masked below
-        const uint32_t x = u_[k][d] + qq[d];
+        const uint32_t x = (c - f_[k][d]) + qq[d];
         uint32_t util;
-        if (!FAST && anyW[d]) {
+        if (anyW) {
           bool nz;
-          const uint32_t t = div_floor32(x, c_[k][d], R_[k][d], k_[k][d], S, nz);
+          const uint32_t t = div_floor32(x, cc, R, kk, S, nz);
           util = MOST ? t : t + (nz ? 1u : 0u);
         } else {
-          uint32_t t = mul_u24(x, R_[k][d]) >> k_[k][d];
-          if (!FAST && MOST && allE[d]) {
+          uint32_t t = mul_u24(x, R) >> kk;
+          if (MOST && allE) {
             util = t;
           } else {
             // r = x*S - t*c lies in [0, 2c) and c < 2^24: exact mod 2^32
-            uint32_t rr = mul_u24(x, S) - mul_u24(t, c_[k][d]);
-            const bool up = rr >= c_[k][d];
+            uint32_t rr = mul_u24(x, S) - mul_u24(t, cc);
+            const bool up = rr >= cc;
             t += up ? 1u : 0u;
-            if (MOST) {
-              util = t;
-            } else {
-              rr -= up ? c_[k][d] : 0u;
-              util = t + (rr != 0u ? 1u : 0u);
-            }
+            rr -= up ? cc : 0u;
+            util = MOST ? t : t + (rr != 0u ? 1u : 0u);
           }
         }
         acc[k] += (int32_t)__umul24((uint32_t)sp.w[d], util);
@@ -289,8 +407,6 @@ __device__ __forceinline__ void score_rows(
     int32_t sv[NPL];
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
-      // GPU-topology fit: the job takes exactly the node's free GPUs;
-      // CacheStrategy shared: the node is in the job's affinity domain
       const int32_t bonus = ((qg != 0u && fg_[k] == qg) ? wfit : 0) + (tp_[k] == af ? waff : 0);
       const int32_t s = (MOST ? acc[k] : b_[k] - acc[k]) + bonus;
       sv[k] = fits[k] ? s : KP_SCORE_INFEASIBLE;
@@ -340,10 +456,14 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
   // per row: the D requests, the request in the GPU dim (0 if none) and the
   // affinity domain (0xFFFFFFFF = none: no node has that domain)
   __shared__ uint32_t sq[kScoreMaxRows][D + 2];
+  // per wave: its uniform capacities ([D] = 1 if the wave is uniform) and,
+  // per row, the thresholds c - rho per dim and WQ (flag kRowNoFit)
+  __shared__ uint32_t scu[4][D + 1];
+  __shared__ uint32_t sx[4][kScoreMaxRows][D + 1];
   const int N = sp.N;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int tile0 = blockIdx.x * (256 * NPL) + wave * (64 * NPL);
-  const int nb = tile0 + lane * NPL;  // first of this lane's NPL nodes
+  const int nb = tile0 + lane * NPL;  // first of this lane's NPL columns
   const int r0 = blockIdx.y * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
   const int g = sp.gpu_dim;
@@ -359,60 +479,101 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
     }
     sq[rr][d] = v;
   }
-  uint32_t f_[NPL][D], u_[NPL][D], c_[NPL][D], R_[NPL][D], k_[NPL][D], fg_[NPL], tp_[NPL];
-  int32_t b_[NPL];
+  const typename V::T *pv = reinterpret_cast<const typename V::T *>(np);
+  const int64_t PV = P / NPL, iv = nb / NPL;  // P % 1024 == 0: the tile is inside
+  uint32_t f_[NPL][D], a_[NPL][D], fg_[NPL], tp_[NPL];
+  int32_t b_[NPL], wa_[NPL];
   bool v_[NPL];
-  bool anyW[D], allE[D];
+  uint32_t cu[D];
+  bool uni = true;
   {
-    const typename V::T *pv = reinterpret_cast<const typename V::T *>(np);
-    const int64_t PV = P / NPL, iv = nb / NPL;  // P % 1024 == 0: the tile is inside
-    typename V::T pl[4 * D + 2];
+    typename V::T pf[D], pc[D], pa[D];
 #pragma unroll
-    for (int i = 0; i < 4 * D + 2; ++i) pl[i] = pv[i * PV + iv];
-    uint32_t wmode[D], nonE[D];
-#pragma unroll
-    for (int d = 0; d < D; ++d) wmode[d] = nonE[d] = 0;
+    for (int d = 0; d < D; ++d) {
+      pf[d] = pv[(kPlanes * d + 0) * PV + iv];
+      pc[d] = pv[(kPlanes * d + 1) * PV + iv];
+      pa[d] = pv[(kPlanes * d + 2) * PV + iv];
+    }
+    const typename V::T pb = pv[(kPlanes * D) * PV + iv], pt = pv[(kPlanes * D + 1) * PV + iv],
+                        pw = pv[(kPlanes * D + 2) * PV + iv];
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
+      v_[k] = nb + k < N;
 #pragma unroll
       for (int d = 0; d < D; ++d) {
-        f_[k][d] = V::at(pl[4 * d], k);
-        u_[k][d] = V::at(pl[4 * d + 1], k);
-        R_[k][d] = V::at(pl[4 * d + 2], k);
-        const uint32_t K = V::at(pl[4 * d + 3], k);
-        k_[k][d] = K & 63u;
-        const uint32_t c = f_[k][d] + u_[k][d];
-        c_[k][d] = c ? c : 1u;  // cap 0: feasible x = 0, t = 0, remainder 0 < 1
-        wmode[d] |= K & kDivW;
-        nonE[d] |= (K & kDivE) ^ kDivE;
+        f_[k][d] = V::at(pf[d], k);
+        a_[k][d] = V::at(pa[d], k);
       }
-      v_[k] = nb + k < N;
-      b_[k] = (int32_t)V::at(pl[4 * D], k);
-      tp_[k] = V::at(pl[4 * D + 1], k);
+      b_[k] = (int32_t)V::at(pb, k);
+      tp_[k] = V::at(pt, k);
+      wa_[k] = (int32_t)V::at(pw, k);
       fg_[k] = 0xFFFFFFFFu;  // free GPUs: never equal to a request when there is no GPU dim
 #pragma unroll
       for (int d = 0; d < D; ++d)
         if (d == g) fg_[k] = f_[k][d];
     }
-    // wave-uniform division form per dim: W (64-bit products) if any node
-    // of the wave needs it, E (no remainder check, MostAllocated) if all do
+    // one capacity per dim for the whole wave (and no padding column)?
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      anyW[d] = __ballot(wmode[d] != 0) != 0;
-      allE[d] = __ballot(nonE[d] != 0) == 0;
+      cu[d] = __builtin_amdgcn_readfirstlane(V::at(pc[d], 0));
+      bool differ = false;
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) differ |= !v_[k] || V::at(pc[d], k) != cu[d];
+      uni &= __ballot(differ) == 0;
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) scu[wave][d] = cu[d];
+      scu[wave][D] = uni && tile0 < Ns ? 1u : 0u;
+    }
+  }
+  __syncthreads();  // requests and the waves' capacities staged
+  {
+    // per (uniform wave, row): q*S = Q*c + rho in every dim, one thread each
+    const int nr = r1 - r0;
+    const uint64_t S = (uint64_t)sp.S;
+    for (int t = threadIdx.x; t < 4 * nr; t += blockDim.x) {
+      const int w = t / nr, rr = t - w * nr;
+      if (!scu[w][D]) continue;
+      uint32_t wq = 0;
+      bool ok = true;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const uint32_t c = scu[w][d], qd = sq[rr][d];
+        uint32_t thr = 0xFFFFFFFFu;  // cap-0 dim: contributes 0, fits only q = 0
+        if (c == 0u) {
+          ok &= qd == 0u;
+        } else if (qd > c) {
+          ok = false;
+        } else {
+          uint64_t Q, rho;
+          udivmod_uniform((uint64_t)qd * S, c, Q, rho);
+          thr = c - (uint32_t)rho;  // in (0, c]: carry iff a >= thr
+          wq += (uint32_t)sp.w[d] * (uint32_t)Q;
+        }
+        sx[w][rr][d] = thr;
+      }
+      sx[w][rr][D] = ok ? wq : kRowNoFit;
     }
   }
   __syncthreads();
-  if (tile0 >= Ns) return;  // wave-uniform, after the only barrier
-  bool slow = false;
-#pragma unroll
-  for (int d = 0; d < D; ++d) slow |= anyW[d];
-  if (!slow)
-    score_rows<D, MOST, NPL, true>(sp, sq, r0, r1, f_, u_, c_, R_, k_, fg_, tp_, b_, v_, anyW,
-                                   allE, score, mask, Ns, tile0, nb, lane);
-  else
-    score_rows<D, MOST, NPL, false>(sp, sq, r0, r1, f_, u_, c_, R_, k_, fg_, tp_, b_, v_, anyW,
-                                    allE, score, mask, Ns, tile0, nb, lane);
+  if (tile0 >= Ns) return;  // wave-uniform, after the last barrier
+#ifdef KP_SCORE_UNIFORM_ONLY_TIMING  // A/B timing of the uniform path alone (wrong on boundary waves)
+  uni = true;
+#endif
+  if (uni) {
+    score_rows_uniform<D, MOST, NPL>(sp, sq, sx[wave], r0, r1, f_, a_, wa_, fg_, tp_, b_, score,
+                                     mask, Ns, tile0, nb, lane);
+    return;
+  }
+  // mixed capacities (a class boundary, padding, or an unclustered cluster):
+  // the per-node division of div_prep. Such waves are few on a clustered
+  // node table, so their node operands are re-read per row (L1/L2) rather
+  // than held in registers the uniform path does not need.
+#ifndef KP_SCORE_UNIFORM_ONLY_TIMING
+  score_rows_mixed<D, MOST, NPL>(sp, sq, r0, r1, pv, PV, iv, f_, fg_, tp_, b_, v_, score, mask, Ns,
+                                 tile0, nb, lane);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -453,7 +614,8 @@ __global__ __launch_bounds__(BS) void k_select_t(ScoreParams sp,
                                                  const int32_t *__restrict__ rows_unit,
                                                  const uint32_t *__restrict__ salt, int32_t rows,
                                                  int32_t lds_cap, int32_t *__restrict__ cand,
-                                                 const int32_t *__restrict__ rows_dev) {
+                                                 const int32_t *__restrict__ rows_dev,
+                                                 const int32_t *__restrict__ perm) {
   constexpr int NW = BS / 64;
   __shared__ uint64_t buf[kSelLdsCap];
   __shared__ uint64_t wth[NW];
@@ -565,7 +727,10 @@ __global__ __launch_bounds__(BS) void k_select_t(ScoreParams sp,
     const uint64_t ki = buf[i];
     int r = 0;
     for (int jj = 0; jj < C; ++jj) r += buf[jj] > ki ? 1 : 0;
-    if (r < K) cand[(int64_t)row * K + r] = key_node(ki, sl, inv);
+    if (r < K) {  // column (canonical position) -> node
+      const int32_t pos = key_node(ki, sl, inv);
+      cand[(int64_t)row * K + r] = perm ? perm[pos] : pos;
+    }
   }
   if (tid >= C && tid < K) cand[(int64_t)row * K + tid] = -1;
 }
@@ -596,7 +761,8 @@ __global__ __launch_bounds__(256) void k_select(ScoreParams sp,
                                                 const int32_t *__restrict__ rows_unit,
                                                 const uint32_t *__restrict__ salt,
                                                 int32_t rows, int32_t *__restrict__ cand,
-                                                const int32_t *__restrict__ rows_dev) {
+                                                const int32_t *__restrict__ rows_dev,
+                                                const int32_t *__restrict__ perm) {
   __shared__ uint64_t part[4][KC];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int row = blockIdx.x;
@@ -652,7 +818,10 @@ __global__ __launch_bounds__(256) void k_select(ScoreParams sp,
   const uint32_t inv = sp.tie_rotated ? kTieMulInv : 1u;
   for (int it = 0; it < K; ++it) {
     const uint64_t m = wave_max_u64(h0);
-    if (lane == 0) cand[(int64_t)row * K + it] = m != 0 ? key_node(m, sl, inv) : -1;
+    if (lane == 0) {  // column (canonical position) -> node
+      const int32_t pos = m != 0 ? key_node(m, sl, inv) : -1;
+      cand[(int64_t)row * K + it] = pos < 0 ? -1 : perm ? perm[pos] : pos;
+    }
     if (m != 0 && h0 == m) {
       h0 = h1;
       h1 = 0;
@@ -849,8 +1018,9 @@ struct ScoreL {
       const int rpb = 32;
       dim3 grid(blocks(Ns, 256 * NPL), blocks(rows, rpb));
       hipLaunchKernelGGL((k_score<D, NPL>), grid, dim3(256), 0, c->stream, sp, c->d.cap,
-                         c->d.used, c->d.topo, q, qstride, c->d.aff, rows_unit, rows, rpb,
-                         c->score_min_rpb, score, mask, Ns, rows_dev);
+                         c->d.used, c->d.topo, c->pack_canonical ? c->d.perm : nullptr, q,
+                         qstride, c->d.aff, rows_unit, rows, rpb, c->score_min_rpb, score, mask,
+                         Ns, rows_dev);
     }
     KP_HIP(hipGetLastError());
     return KP_OK;
@@ -886,13 +1056,13 @@ int launch_score(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int
 namespace {
 using SelFn = void (*)(dim3, hipStream_t, const ScoreParams &, const int32_t *, int32_t,
                        const int32_t *, const uint32_t *, int32_t, int32_t, int32_t *,
-                       const int32_t *);
+                       const int32_t *, const int32_t *);
 template <int V4, int BS>
 void sel_t(dim3 grid, hipStream_t st, const ScoreParams &sp, const int32_t *score, int32_t Ns,
            const int32_t *rows_unit, const uint32_t *salt, int32_t rows, int32_t cap,
-           int32_t *cand, const int32_t *rows_dev) {
+           int32_t *cand, const int32_t *rows_dev, const int32_t *perm) {
   hipLaunchKernelGGL((k_select_t<V4, BS>), grid, dim3(BS), 0, st, sp, score, Ns, rows_unit, salt,
-                     rows, cap, cand, rows_dev);
+                     rows, cap, cand, rows_dev, perm);
 }
 struct SelShape {
   int v4, bs;
@@ -937,19 +1107,20 @@ int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, in
   const SelShape *sh = c->select_generic ? nullptr : sel_shape(Ns, pref);
   if (!sh && !c->select_generic) sh = sel_shape(Ns, 0);
   if (sh) {
-    sh->fn(grid, c->stream, sp, score, Ns, rows_unit, c->d.salt, rows, cap, cand, rows_dev);
+    sh->fn(grid, c->stream, sp, score, Ns, rows_unit, c->d.salt, rows, cap, cand, rows_dev,
+           c->d.perm);
   } else if (K <= 4) {
     hipLaunchKernelGGL(k_select<4>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
-                       c->d.salt, rows, cand, rows_dev);
+                       c->d.salt, rows, cand, rows_dev, c->d.perm);
   } else if (K <= 8) {
     hipLaunchKernelGGL(k_select<8>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
-                       c->d.salt, rows, cand, rows_dev);
+                       c->d.salt, rows, cand, rows_dev, c->d.perm);
   } else if (K <= 16) {
     hipLaunchKernelGGL(k_select<16>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
-                       c->d.salt, rows, cand, rows_dev);
+                       c->d.salt, rows, cand, rows_dev, c->d.perm);
   } else {
     hipLaunchKernelGGL(k_select<32>, grid, dim3(256), 0, c->stream, sp, score, Ns, rows_unit,
-                       c->d.salt, rows, cand, rows_dev);
+                       c->d.salt, rows, cand, rows_dev, c->d.perm);
   }
   KP_HIP(hipGetLastError());
   return KP_OK;
@@ -962,8 +1133,9 @@ struct RoundStartL {
     const int64_t n = std::max<int64_t>(hi - lo, P);
     if (n <= 0) return KP_OK;
     hipLaunchKernelGGL((k_round_start<D>), dim3(blocks(n, 256)), dim3(256), 0, c->stream,
-                       c->d.status, lo, hi, flag, c->d.cap, c->d.used, c->d.R32, c->d.K32,
-                       c->d.base, c->d.topo, c->N, P, c->d.np32);
+                       c->d.status, lo, hi, flag, c->d.cap, c->d.used, c->d.base, c->d.topo,
+                       c->pack_canonical ? c->d.perm : nullptr, c->N, P, c->pack_sp,
+                       c->d.np32);
     KP_HIP(hipGetLastError());
     return KP_OK;
   }

@@ -28,6 +28,8 @@ struct kpo_state {
   const int64_t *cap;
   int64_t *used;      /* [D*N] committed usage                               */
   int32_t *topo;      /* [N]                                                 */
+  int32_t *pos;       /* [N] canonical position: rank of the node in the
+                         order (cap vector lexicographic, node index) (§2.3) */
   /* units in rank order (§2.2) */
   int32_t U;
   int32_t *leader;    /* [U] first job index                                 */
@@ -86,9 +88,13 @@ static uint32_t fmix32(uint32_t h) {
   h ^= h >> 16;
   return h;
 }
+/* The tie key is a function of the node's canonical position pos(n): the
+   rank of n when the nodes are sorted by (cap[0], ..., cap[D-1], n). Nodes
+   with the same capacities keep index order, so "lowest index" still holds
+   among identical nodes. */
 static uint32_t tie_key(const kpo_state *st, int32_t u, int32_t n) {
-  if (st->p.tie_mode == KP_TIE_NODE_INDEX) return (uint32_t)n;
-  return (uint32_t)n * 0x9E3779B1u + st->salt[u];
+  if (st->p.tie_mode == KP_TIE_NODE_INDEX) return (uint32_t)st->pos[n];
+  return (uint32_t)st->pos[n] * 0x9E3779B1u + st->salt[u];
 }
 
 /* ---- §2.3 filter + score ---------------------------------------------------
@@ -146,6 +152,16 @@ static int cmp_rank(const void *a, const void *b) {
     return g_prio_sort[x] > g_prio_sort[y] ? -1 : 1; /* prio desc */
   return g_lead_sort[x] < g_lead_sort[y] ? -1 : (g_lead_sort[x] > g_lead_sort[y]);
 }
+static const int64_t *g_cap_sort; /* qsort context: cap [D*N] */
+static int32_t g_cap_D, g_cap_N;
+static int cmp_canon(const void *a, const void *b) {
+  int32_t x = *(const int32_t *)a, y = *(const int32_t *)b;
+  for (int d = 0; d < g_cap_D; ++d) {
+    int64_t cx = g_cap_sort[(int64_t)d * g_cap_N + x], cy = g_cap_sort[(int64_t)d * g_cap_N + y];
+    if (cx != cy) return cx < cy ? -1 : 1;
+  }
+  return x < y ? -1 : (x > y);
+}
 static int cmp_i32(const void *a, const void *b) {
   int32_t x = *(const int32_t *)a, y = *(const int32_t *)b;
   return x < y ? -1 : (x > y);
@@ -153,7 +169,7 @@ static int cmp_i32(const void *a, const void *b) {
 
 void kpo_state_free(kpo_state *st) {
   if (!st) return;
-  free(st->used); free(st->topo); free(st->aff);
+  free(st->used); free(st->topo); free(st->aff); free(st->pos);
   free(st->leader); free(st->size); free(st->salt);
   free(st->status); free(st->prio); free(st->job_node); free(st->job_score);
   free(st);
@@ -189,6 +205,17 @@ int kpo_state_new(const kp_snapshot *s, const kp_params *p, kpo_state **out) {
   }
   for (int64_t i = 0; i < (int64_t)D * N; ++i) st->used[i] = s->used ? s->used[i] : 0;
   for (int32_t n = 0; n < N; ++n) st->topo[n] = s->topo_domain ? s->topo_domain[n] : n;
+  { /* canonical positions (§2.3 tie keys) */
+    int32_t *ord;
+    XALLOC(ord, N, int32_t);
+    XALLOC(st->pos, N, int32_t);
+    if (!ord || !st->pos) { free(ord); free(uleader); free(usize); free(uprio); free(uaff); kpo_state_free(st); return KP_ENOMEM; }
+    for (int32_t n = 0; n < N; ++n) ord[n] = n;
+    g_cap_sort = s->cap; g_cap_D = D; g_cap_N = N;
+    qsort(ord, N, sizeof(int32_t), cmp_canon);
+    for (int32_t i = 0; i < N; ++i) st->pos[ord[i]] = i;
+    free(ord);
+  }
   for (int32_t j = 0; j < J; ++j) { st->job_node[j] = -1; st->job_score[j] = KP_SCORE_NONE; }
 
   /* units: maximal runs of equal gang_id >= 0; gang_id < 0 stands alone */

@@ -75,8 +75,14 @@ def place(req, cap, used, prio, gang_id, topo, p, affinity=None):
             s += p.get("w_affinity", 0)
         return s
 
+    # canonical position: rank in the order (cap vector, node index)
+    order = sorted(range(N), key=lambda n: (tuple(cap[d][n] for d in range(D)), n))
+    pos = [0] * N
+    for i, n in enumerate(order):
+        pos[n] = i
+
     def tie(u, n):
-        return n if p["tie_mode"] == 0 else (n * TIE_MUL + salt[u]) & MASK32
+        return pos[n] if p["tie_mode"] == 0 else (pos[n] * TIE_MUL + salt[u]) & MASK32
 
     def q_of(u):
         return [req[d][units[u][0]] for d in range(D)]

@@ -109,7 +109,7 @@ def test_config1_batch_runner_with_oracle(oracle):
             assert c["message"].count("->") == reps
         else:
             assert c["reason"] in ("NoFit", "RoundLimit")
-    assert placed > 50 and summary["placed"] > 0
+    assert placed >= 40 and summary["placed"] > 0  # the cluster is ~2x oversubscribed in GPUs
     assert m.assigned.labels("placed")._value.get() == summary["placed"]
     # deterministic: the same snapshot gives the same statuses (fail-over safety)
     _, _, written2, _, _ = run_config1(OraclePlacer(oracle))

@@ -1,18 +1,21 @@
 #!/bin/bash
-# Build libkplace.so of git revision $1 (or "WORKTREE" = the working tree) into
-# kubernetes-native-distributed-ai-job-scheduler_amd/build/ab/$2.so for tools/ab_libs.sh.
+# Build libkplace.so of git revision $1 (or "WORKTREE" = the working tree)
+# into kubernetes-native-distributed-ai-job-scheduler_amd/build/ab/$2.so for
+# tools/ab_libs.sh / tools/ab_frac.sh; $3 = extra compiler flags (e.g. -DX).
 set -e
 REPO=$(cd "$(dirname "$0")/.." && pwd)
-OUT=$REPO/kubernetes-native-distributed-ai-job-scheduler_amd/build/ab
+PKG=kubernetes-native-distributed-ai-job-scheduler_amd
+OUT=$REPO/$PKG/build/ab
 mkdir -p "$OUT"
+WT=$(mktemp -d /tmp/kpwt.XXXX)
 if [ "$1" = WORKTREE ]; then
-  make -s -C "$REPO/kubernetes-native-distributed-ai-job-scheduler_amd" -j8 >/dev/null
-  cp "$REPO/kubernetes-native-distributed-ai-job-scheduler_amd/libkplace.so" "$OUT/$2.so"
+  mkdir -p "$WT/$PKG"
+  cp -r "$REPO/include" "$WT/"
+  cp -r "$REPO/$PKG/csrc" "$REPO/$PKG/Makefile" "$WT/$PKG/"
 else
-  WT=$(mktemp -d /tmp/kpwt.XXXX)
   git -C "$REPO" worktree add -q --detach "$WT" "$1"
-  make -s -C "$WT/kubernetes-native-distributed-ai-job-scheduler_amd" -j8 >/dev/null
-  cp "$WT/kubernetes-native-distributed-ai-job-scheduler_amd/libkplace.so" "$OUT/$2.so"
-  git -C "$REPO" worktree remove --force "$WT"
 fi
+make -s -C "$WT/$PKG" -j8 CXXFLAGS="-O3 -std=c++17 -fPIC -pthread -Wall -Wno-unused-result $3" >/dev/null
+cp "$WT/$PKG/libkplace.so" "$OUT/$2.so"
+if [ "$1" = WORKTREE ]; then rm -rf "$WT"; else git -C "$REPO" worktree remove --force "$WT"; fi
 echo "built $OUT/$2.so"
