@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 2
+#define KP_ABI_VERSION 3
 
 /* ---- limits ------------------------------------------------------------ */
 #define KP_MAX_DIMS 8       /* resource dimensions per job/node               */
@@ -261,6 +261,9 @@ typedef struct kp_timing {
   int64_t score_launches;
   int64_t score_bytes;      /* algorithmic bytes of the filter+score kernels */
   int64_t select_bytes;     /* algorithmic bytes of the select kernels       */
+  int32_t fused;            /* 1: fused filter+score+top-K (no score matrix;
+                               score_* then time/count k_score_topk)         */
+  int32_t reserved;
 } kp_timing;
 int kp_last_timing(kp_ctx *ctx, kp_timing *t);
 

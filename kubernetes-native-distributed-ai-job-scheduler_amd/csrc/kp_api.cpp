@@ -128,8 +128,27 @@ static int ensure_nodes(kp_ctx *c, int32_t N, int32_t D) {
   // +4: k_accept's list mode reads node_list[wave] for up to 3 padding waves
   KP_TRY(dalloc(&c->d.node_list, (size_t)n + 4));
   KP_TRY(dalloc(&c->d.perm, (size_t)n));
-  KP_TRY(dalloc(&c->d.np32, (size_t)(5 * D + 3) * (((size_t)n + 1023) & ~(size_t)1023)));
   c->cap_N = n;
+  return KP_OK;
+}
+
+// 32-bit node planes: [5*D+3][cols], cols = the widest layout in use (the
+// fused solve's class-aligned columns or round_up(N, 1024))
+static int ensure_np32(kp_ctx *c, int64_t cols, int32_t D) {
+  const int64_t need = (int64_t)(5 * D + 3) * std::max<int64_t>(cols, 1024);
+  if (c->d.np32 && need <= c->cap_P) return KP_OK;
+  c->cap_P = 0;
+  KP_TRY(dalloc(&c->d.np32, (size_t)need));
+  c->cap_P = need;
+  return KP_OK;
+}
+
+// per-tile top-K lists of the fused solve: rows x tiles x K keys
+static int ensure_part(kp_ctx *c, int64_t entries) {
+  if (c->d.part && entries <= c->cap_part) return KP_OK;
+  c->cap_part = 0;
+  KP_TRY(dalloc(&c->d.part, (size_t)std::max<int64_t>(entries, 64)));
+  c->cap_part = entries;
   return KP_OK;
 }
 
@@ -307,6 +326,8 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = std::getenv("KP_SCORE_MIN_RPB")) c->score_min_rpb = std::max(1, std::atoi(e));
   if (const char *e = std::getenv("KP_SCORE_NPL")) c->score_npl = std::atoi(e) == 4 ? 4 : 2;
   if (const char *e = std::getenv("KP_COMPACT_MAX")) c->compact_max = std::atoi(e);
+  if (const char *e = std::getenv("KP_FUSED")) c->fused_enabled = std::atoi(e) != 0;
+  if (const char *e = std::getenv("KP_FZ_WG_TARGET")) c->fz_wg_target = std::max(64, std::atoi(e));
   if (hipSetDevice(dev) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void **>(&c->pinned), 4096, hipHostMallocDefault) !=
@@ -375,7 +396,55 @@ static int load_nodes_impl(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap,
   } catch (const std::bad_alloc &) {
     return fail(KP_ENOMEM, "kp_load_nodes: host copy");
   }
+  // class-aligned layout of the fused solve (kp_topk.hip): each run of equal
+  // capacity vectors in canonical order starts on a 128-column wave tile
+  std::vector<int32_t> colnode, wshift;
+  int64_t fz_cols = 0;
+  try {
+    auto same = [&](int32_t a, int32_t b) {
+      for (int d = 0; d < D; ++d)
+        if (cap[(int64_t)d * N + a] != cap[(int64_t)d * N + b]) return false;
+      return true;
+    };
+    std::vector<std::pair<int32_t, int32_t>> cls;  // (first position, length)
+    for (int32_t i = 0; i < N;) {
+      int32_t e = i + 1;
+      while (e < N && same(c->h_perm[e], c->h_perm[i])) ++e;
+      cls.emplace_back(i, e - i);
+      fz_cols = ((fz_cols + 127) & ~(int64_t)127) + (e - i);
+      i = e;
+    }
+    const int64_t P = (std::max<int64_t>(fz_cols, 1) + 1023) & ~(int64_t)1023;
+    if (N > 0 && P <= ((int64_t)1 << 24)) {
+      colnode.assign((size_t)P, -1);
+      wshift.assign((size_t)(P / 128), 0);
+      int64_t col = 0;
+      for (const auto &cl : cls) {
+        col = (col + 127) & ~(int64_t)127;
+        for (int64_t t = col; t < col + cl.second; t += 128)
+          wshift[(size_t)(t / 128)] = (int32_t)(col - cl.first);
+        for (int32_t k = 0; k < cl.second; ++k) colnode[(size_t)(col + k)] = c->h_perm[cl.first + k];
+        col += cl.second;
+      }
+    }
+  } catch (const std::bad_alloc &) {
+    return fail(KP_ENOMEM, "kp_load_nodes: host copy");
+  }
+  const int32_t fz_P = (int32_t)colnode.size();
   KP_TRY(ensure_nodes(c, N, D));
+  KP_TRY(ensure_np32(c, std::max<int64_t>(fz_P, ((int64_t)N + 1023) & ~(int64_t)1023), D));
+  if (fz_P > 0) {
+    if ((int64_t)fz_P > c->cap_fz) {
+      c->cap_fz = 0;
+      KP_TRY(dalloc(&c->d.colnode, (size_t)fz_P));
+      KP_TRY(dalloc(&c->d.wshift, (size_t)fz_P / 128));
+      c->cap_fz = fz_P;
+    }
+    KP_HIP(hipMemcpyAsync(c->d.colnode, colnode.data(), sizeof(int32_t) * fz_P,
+                          hipMemcpyHostToDevice, c->stream));
+    KP_HIP(hipMemcpyAsync(c->d.wshift, wshift.data(), sizeof(int32_t) * (fz_P / 128),
+                          hipMemcpyHostToDevice, c->stream));
+  }
   if (N > 0) {
     KP_HIP(hipMemcpyAsync(c->d.cap, c->h_cap.data(), sizeof(int64_t) * D * N,
                           hipMemcpyHostToDevice, c->stream));
@@ -394,8 +463,13 @@ static int load_nodes_impl(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap,
   c->R = 0;
   c->N = N;
   c->D = D;
-  c->caps32 = true;
-  for (int64_t i = 0; i < (int64_t)D * N; ++i) c->caps32 = c->caps32 && cap[i] < ((int64_t)1 << 32);
+  c->max_cap = 0;
+  for (int64_t i = 0; i < (int64_t)D * N; ++i) c->max_cap = std::max(c->max_cap, cap[i]);
+  c->caps32 = c->max_cap < ((int64_t)1 << 32);
+  // the fused layout pays off while the padding stays small (few capacity
+  // classes); the merge holds at most 2,048 keys per row (tiles x K)
+  c->fz_P = fz_P;
+  c->fz_layout_ok = fz_P > 0 && fz_cols - N <= N / 8 + 1024;
   c->fits32 = c->caps32 && c->reqs32 && c->jobs_loaded;
   c->util_scale_loaded = 0;  // force a division-table rebuild at the next solve
   c->nodes_loaded = true;
@@ -497,8 +571,9 @@ static int load_jobs_impl(kp_ctx *c, int32_t J, const int64_t *req, const int32_
   // this rank's shard: a contiguous block of rank positions
   c->u_lo = (int32_t)((int64_t)U * c->rank / c->world);
   c->u_hi = (int32_t)((int64_t)U * (c->rank + 1) / c->world);
-  c->reqs32 = true;
-  for (int64_t i = 0; i < (int64_t)D * J; ++i) c->reqs32 = c->reqs32 && req[i] < ((int64_t)1 << 32);
+  c->max_req = 0;
+  for (int64_t i = 0; i < (int64_t)D * J; ++i) c->max_req = std::max(c->max_req, req[i]);
+  c->reqs32 = c->max_req < ((int64_t)1 << 32);
   c->fits32 = c->caps32 && c->reqs32;
   c->jobs_loaded = true;
   return KP_OK;
@@ -578,9 +653,32 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   KP_TRY(launch_reset_units(c));
   c->pack_sp = sp;
   c->pack_canonical = true;  // the solve scores in canonical column order
-  const int64_t rpc = rows_per_chunk(c);
   const int32_t shard = c->u_hi - c->u_lo;
-  KP_TRY(ensure_matrix(c, (int32_t)std::min<int64_t>(std::max(shard, 1), rpc)));
+  // Fused filter + score + top-K (kp_topk.hip) when the class-aligned layout
+  // is compact and every operand and score fits its 31-bit / 32-bit key
+  // field; else the materialised score matrix + top-K select.
+  int32_t ksh = 0;
+  {
+    int64_t bound = (int64_t)p->w_gpu_fit + p->w_affinity + 1;
+    for (int d = 0; d < c->D; ++d) bound += (int64_t)p->w_dim[d] * p->util_scale;
+    int bits = 0;
+    while (bits < 63 && (bound >> bits) != 0) ++bits;
+    ksh = 32 - bits;  // (score + 1) << ksh keeps the score; >= 8 tie-key bits below it
+  }
+  const bool fused = c->fused_enabled && c->fz_layout_ok && c->fits32 &&
+                     c->max_cap < ((int64_t)1 << 31) && c->max_req < ((int64_t)1 << 31) &&
+                     ksh >= 8 && (int64_t)(c->fz_P / 1024) * K <= 2048;
+  c->pack_fused = fused;
+  c->last_fused = fused;
+  int64_t rpc = rows_per_chunk(c);
+  if (fused) {
+    rpc = INT64_MAX;  // no matrix, no chunks: per row only tiles x K keys
+    KP_TRY(ensure_part(c, (int64_t)std::max(shard, 1) * (c->fz_P / 1024) * K));
+    if (!c->d.part || !c->d.colnode || !c->d.wshift)
+      return fail(KP_ENOMEM, "kp_solve: a fused-path buffer is missing");
+  } else {
+    KP_TRY(ensure_matrix(c, (int32_t)std::min<int64_t>(std::max(shard, 1), rpc)));
+  }
 
   Events E;  // every event of this solve, destroyed on every exit path
   // timing-only events: no system-scope fence (cache writeback/invalidate)
@@ -614,14 +712,20 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     // the solve needs only the score matrix: its -1 sentinel is the
     // feasibility filter, so the bit mask (kp_score's second output) is not
     // materialised here
-    KP_TRY(launch_score(c, sp, c->d.act_local + r0, rows, c->d.score, nullptr, c->d.q, U,
-                        rows_dev));
+    if (fused) {
+      KP_TRY(launch_score_topk(c, sp, c->d.act_local + r0, rows, ksh, c->d.cand_local + r0 * K,
+                               rows_dev));
+    } else {
+      KP_TRY(launch_score(c, sp, c->d.act_local + r0, rows, c->d.score, nullptr, c->d.q, U,
+                          rows_dev));
+    }
     if (c->profiling) {
       KP_HIP(hipEventRecord(ke.b, c->stream));
       kev.push_back(ke);
     }
-    KP_TRY(launch_select(c, sp, c->d.act_local + r0, rows, c->d.score, c->d.cand_local + r0 * K,
-                         rows_dev));
+    if (!fused)
+      KP_TRY(launch_select(c, sp, c->d.act_local + r0, rows, c->d.score,
+                           c->d.cand_local + r0 * K, rows_dev));
     tm.score_launches++;
     return KP_OK;
   };
@@ -729,11 +833,19 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     int64_t rows = ke.rows_bound;
     if (ke.round < (int32_t)round_active.size())
       rows = std::min<int64_t>(rows, round_active[ke.round]);
-    tm.score_bytes += rows * Ns * 4 + (int64_t)8 * c->D * rows + (int64_t)3 * 8 * c->D * N +
-                      8 * (int64_t)N;
-    tm.select_bytes += rows * Ns * 4 + rows * K * 4;
+    if (fused) {  // compulsory bytes: requests in, per-tile lists out, node planes once
+      const int64_t lists = (int64_t)(c->fz_P / 1024) * K * 8;
+      tm.score_bytes += rows * ((int64_t)8 * c->D + 12 + lists) +
+                        (int64_t)(2 * c->D + 3) * 4 * c->fz_P;
+      tm.select_bytes += rows * (lists + K * 4);  // k_merge_topk
+    } else {
+      tm.score_bytes += rows * Ns * 4 + (int64_t)8 * c->D * rows + (int64_t)3 * 8 * c->D * N +
+                        8 * (int64_t)N;
+      tm.select_bytes += rows * Ns * 4 + rows * K * 4;
+    }
   }
   tm.accept_ms = tm.solve_ms - tm.score_ms - tm.select_ms;
+  tm.fused = fused ? 1 : 0;
   c->timing = tm;
   int32_t placed = 0;
   for (int32_t u = 0; u < U; ++u)
@@ -877,7 +989,7 @@ void kp_destroy(kp_ctx *c) {
                   d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
                   d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.roff,
                   d.rreq, d.rsuf, d.rprio, d.pre_node, d.pre_vict, d.pre_cost,
-                  d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.stats, d.np32};
+                  d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.stats, d.np32, d.colnode, d.wshift, d.part};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->world > 1) {
@@ -1057,6 +1169,7 @@ int kp_score(kp_ctx *c, const kp_params *p, int32_t job_lo, int32_t job_hi, int3
   std::vector<uint64_t> hm;
   c->pack_sp = sp;
   c->pack_canonical = false;  // kp_score returns columns in node order
+  c->pack_fused = false;
   KP_TRY(launch_pack(c));  // 32-bit node planes of the current usage
   for (int64_t r0 = 0; r0 < rows; r0 += rpc) {
     const int32_t nr = (int32_t)std::min<int64_t>(rpc, rows - r0);

@@ -48,6 +48,30 @@ __device__ __forceinline__ int64_t dpp_i64(int64_t v) {
   const uint32_t h2 = (uint32_t)__builtin_amdgcn_mov_dpp(hi, CTRL, 0xf, 0xf, false);
   return (int64_t)(((uint64_t)h2 << 32) | l2);
 }
+// 64-bit wave max, result in every lane: DPP max inside each 16-lane row
+// (row_shr 1/2/4/8: lane 15 of a row ends with the row max), then the four
+// row maxima through scalar readlanes (VALU-only, no LDS crossbar)
+__device__ __forceinline__ uint64_t wave_max_u64_dpp(uint64_t v) {
+  const int rl16 = __lane_id() & 15;
+  uint64_t t;
+  t = (uint64_t)dpp_i64<0x111>((int64_t)v);
+  if (rl16 >= 1 && t > v) v = t;
+  t = (uint64_t)dpp_i64<0x112>((int64_t)v);
+  if (rl16 >= 2 && t > v) v = t;
+  t = (uint64_t)dpp_i64<0x114>((int64_t)v);
+  if (rl16 >= 4 && t > v) v = t;
+  t = (uint64_t)dpp_i64<0x118>((int64_t)v);
+  if (rl16 >= 8 && t > v) v = t;
+  uint64_t m = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 16 * r + 15);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 16 * r + 15);
+    const uint64_t x = ((uint64_t)hi << 32) | lo;
+    m = x > m ? x : m;
+  }
+  return m;
+}
 // inclusive prefix sum over the 64 lanes with DPP (row_shr 1/2/4/8 inside
 // each 16-lane row, then row_bcast 15/31 across rows): VALU-only, no LDS
 // crossbar round trips
@@ -296,6 +320,40 @@ __device__ __forceinline__ int32_t group_max_i32(int32_t v) {
   return __builtin_amdgcn_readlane(v, 63);
 }
 
+// u32 planes per dim of the packed 32-bit node tile (kp_score.hip pack_node)
+constexpr int kPlanes = 5;
+
+__device__ __forceinline__ void fit_rows(int32_t act, int32_t min_rpb, int32_t &rows,
+                                         int32_t &rows_per_block) {
+  rows = min(rows, act);
+  const int32_t even = (rows + (int32_t)gridDim.y - 1) / (int32_t)gridDim.y;
+  rows_per_block = min(rows_per_block, max(min_rpb, even));
+}
+
+// floor(n / c) and n mod c for a 64-bit n < 2^53 and c > 0: a double
+// estimate corrected by one step each way
+__device__ __forceinline__ void udivmod_uniform(uint64_t n, uint32_t c, uint64_t &Q, uint64_t &r) {
+  Q = (uint64_t)((double)n / (double)c);
+  int64_t rr = (int64_t)n - (int64_t)(Q * c);
+  if (rr < 0) {
+    --Q;
+    rr += c;
+  } else if (rr >= (int64_t)c) {
+    ++Q;
+    rr -= c;
+  }
+  r = (uint64_t)rr;
+}
+
+// Candidate keys: (valid bit | score | ~tie key), unique per node because the
+// tie key is a bijection of the canonical position. Larger = better.
+__device__ __forceinline__ uint64_t pack_key(int32_t s, uint32_t tk) {
+  return (1ull << 63) | ((uint64_t)(uint32_t)s << 32) | (uint64_t)(~tk);
+}
+__device__ __forceinline__ int32_t key_node(uint64_t key, uint32_t sl, uint32_t inv) {
+  const uint32_t tk = ~(uint32_t)key;
+  return (int32_t)((tk - sl) * inv);
+}
 inline int blocks(int64_t n, int b) { return (int)((n + b - 1) / b); }
 
 template <template <int> class F, typename... Args>

@@ -57,7 +57,14 @@ struct DevState {
   int64_t *base = nullptr;  // LeastAllocated base: sum of w*S over dims with cap > 0
   int32_t *topo = nullptr;
   int32_t *perm = nullptr;  // [N] canonical order: nodes sorted by (cap vector, index)
-  uint32_t *np32 = nullptr;  // [5*D+3][round_up(N,1024)] 32-bit score tile planes
+  uint32_t *np32 = nullptr;  // [5*D+3][cap_P] 32-bit score tile planes
+  // fused solve layout: canonical order with every capacity
+  // class starting on a 128-column wave tile; column -> node (-1 = padding)
+  // and per wave tile the canonical position of its first column minus that
+  // column (pos = column - wshift[column / 128])
+  int32_t *colnode = nullptr;  // [fz_P]
+  int32_t *wshift = nullptr;   // [fz_P / 128]
+  uint64_t *part = nullptr;    // [rows][fz_P / 1024][K] per-tile top-K keys
   // units (rank order), job outputs
   int64_t *q = nullptr;  // [D][U]
   int32_t *leader = nullptr, *size = nullptr, *status = nullptr;
@@ -146,12 +153,21 @@ struct kp_ctx {
   // score launch geometry (tuning knobs): target workgroups per launch and
   // the smallest number of job rows per workgroup
   int32_t score_wg_target = 4096, score_min_rpb = 4, score_npl = 2;
+  int32_t fz_wg_target = 2048;  // KP_FZ_WG_TARGET: target workgroups of k_score_topk
   // KP_COMPACT_MAX: largest unit range compacted by the one-workgroup kernel
   int32_t compact_max = 262144;
   // sizes
   int32_t N = 0, D = 0, J = 0, U = 0, R = 0, cap_R = 0, cap_delta = 0;
   int32_t cap_N = 0, cap_U = 0, cap_J = 0, cap_rows = 0, cap_props = 0, cap_K = 0;
   int32_t mat_Ns = 0;          // row stride the score matrix was allocated for
+  int64_t cap_P = 0;           // columns of d.np32
+  int64_t cap_part = 0;        // entries of d.part
+  int64_t cap_fz = 0;          // columns of d.colnode
+  // fused score + top-K (k_score_topk): columns of the class-aligned layout,
+  // whether that layout is compact enough to use, KP_FUSED=0 disables it
+  int32_t fz_P = 0;
+  bool fz_layout_ok = false, fused_enabled = true;
+  int64_t max_cap = 0, max_req = 0;  // largest cap / request of the loaded tables
   int32_t cap_mask_rows = 0;   // rows of d.mask (kp_score only)
   int64_t cap_q = 0;           // int64 entries of d.q
   int32_t u_lo = 0, u_hi = 0;  // this rank's shard of units (rank positions)
@@ -173,6 +189,8 @@ struct kp_ctx {
   // (scores by perm[column]) or kp_score's node order, for these params
   kp::ScoreParams pack_sp{};
   bool pack_canonical = false;
+  bool pack_fused = false;  // the fused layout (colnode), else perm / identity
+  bool last_fused = false;  // the last solve ran the fused candidate phase
   std::vector<int32_t> h_perm;
   kp_result last{};
   kp_timing timing{};
@@ -195,6 +213,10 @@ int launch_score(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit,
 int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit,
                   int32_t rows, const int32_t *score, int32_t *cand,
                   const int32_t *rows_dev = nullptr);
+// fused filter + score + top-K of the solve (kp_topk.hip): candidates of
+// `rows` rows (act_local order) straight into cand, no score matrix
+int launch_score_topk(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
+                      int32_t ksh, int32_t *cand, const int32_t *rows_dev = nullptr);
 int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev = nullptr);
 int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass,
                 const int32_t *A_dev = nullptr);

@@ -55,13 +55,6 @@ __global__ void k_prep_nodes(const int64_t *__restrict__ cap, uint32_t *__restri
 // fills the chip instead of leaving most blocks idle and the rest long.
 // rows_per_block only shrinks (the LDS request stage stays in bounds) and
 // gridDim.y * rpb >= rows holds either way.
-__device__ __forceinline__ void fit_rows(int32_t act, int32_t min_rpb, int32_t &rows,
-                                         int32_t &rows_per_block) {
-  rows = min(rows, act);
-  const int32_t even = (rows + (int32_t)gridDim.y - 1) / (int32_t)gridDim.y;
-  rows_per_block = min(rows_per_block, max(min_rpb, even));
-}
-
 template <int D, int NPL>
 __global__ __launch_bounds__(256) void k_score(ScoreParams sp,
                                                const int64_t *__restrict__ cap,
@@ -161,18 +154,23 @@ __device__ __forceinline__ uint32_t mul_u24(uint32_t a, uint32_t b) {
 // 5D+1, 5D+2; P = round_up(N, 1024) (whole score tiles; padding columns are
 // zero and masked). One 8- or 16-B load per lane and plane fetches a lane's
 // consecutive columns.
-constexpr int kPlanes = 5;  // u32 planes per dim
 
 template <int D>
 __device__ __forceinline__ void pack_node(const int64_t *__restrict__ cap,
                                           const int64_t *__restrict__ used,
                                           const int64_t *__restrict__ base,
                                           const int32_t *__restrict__ topo,
-                                          const int32_t *__restrict__ perm, int32_t N, int32_t P,
-                                          const ScoreParams &sp, uint32_t *__restrict__ np,
-                                          int i) {
-  const bool v = i < N;
-  const int n = v ? (perm ? perm[i] : i) : 0;
+                                          const int32_t *__restrict__ perm,
+                                          const int32_t *__restrict__ colnode, int32_t N,
+                                          int32_t P, const ScoreParams &sp,
+                                          uint32_t *__restrict__ np, int i) {
+  // colnode (the fused solve's class-aligned layout): column -> node, -1 =
+  // padding; the free plane of dim 0 then holds free + 1 (0 on padding), so
+  // that the fused kernel's fit test also rejects padding columns
+  const int cn = colnode ? colnode[i] : 0;
+  const bool v = colnode ? cn >= 0 : i < N;
+  const int n = !v ? 0 : colnode ? cn : perm ? perm[i] : i;
+  const uint32_t plus1 = colnode && v ? 1u : 0u;
   const uint64_t S = (uint64_t)sp.S;
   uint32_t wa = 0;
 #pragma unroll
@@ -188,7 +186,7 @@ __device__ __forceinline__ void pack_node(const int64_t *__restrict__ cap,
     uint32_t R = 0, K = 1u | kDivE;
     div_prep(cc, (uint32_t)S, R, K);
     wa += (uint32_t)sp.w[d] * (uint32_t)A;
-    np[(int64_t)(kPlanes * d + 0) * P + i] = (uint32_t)(cc - uu);
+    np[(int64_t)(kPlanes * d + 0) * P + i] = (uint32_t)(cc - uu) + (d == 0 ? plus1 : 0u);
     np[(int64_t)(kPlanes * d + 1) * P + i] = (uint32_t)cc;
     np[(int64_t)(kPlanes * d + 2) * P + i] = (uint32_t)a;
     np[(int64_t)(kPlanes * d + 3) * P + i] = R;
@@ -210,12 +208,13 @@ __global__ __launch_bounds__(256) void k_round_start(const int32_t *__restrict__
                                                      const int64_t *__restrict__ used,
                                                      const int64_t *__restrict__ base,
                                                      const int32_t *__restrict__ topo,
-                                                     const int32_t *__restrict__ perm, int32_t N,
+                                                     const int32_t *__restrict__ perm,
+                                                     const int32_t *__restrict__ colnode, int32_t N,
                                                      int32_t P, ScoreParams sp,
                                                      uint32_t *__restrict__ np) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < hi - lo) flag[i] = status[lo + i] == kActive ? 1 : 0;
-  if (i < P) pack_node<D>(cap, used, base, topo, perm, N, P, sp, np, i);
+  if (i < P) pack_node<D>(cap, used, base, topo, perm, colnode, N, P, sp, np, i);
 }
 
 // bit j of a 32-bit value -> bit 2j
@@ -243,21 +242,6 @@ struct Vec<4> {
     return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
   }
 };
-
-// floor(n / c) and n mod c for a 64-bit n < 2^53 and c > 0: a double
-// estimate corrected by one step each way
-__device__ __forceinline__ void udivmod_uniform(uint64_t n, uint32_t c, uint64_t &Q, uint64_t &r) {
-  Q = (uint64_t)((double)n / (double)c);
-  int64_t rr = (int64_t)n - (int64_t)(Q * c);
-  if (rr < 0) {
-    --Q;
-    rr += c;
-  } else if (rr >= (int64_t)c) {
-    ++Q;
-    rr -= c;
-  }
-  r = (uint64_t)rr;
-}
 
 // Row loop of a wave whose columns all have the same capacity in every dim
 // (the canonical node order groups equal capacity vectors, so on a cluster
@@ -577,16 +561,8 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
 }
 
 // ---------------------------------------------------------------------------
-// Candidate keys: (valid bit | score | ~tie key), unique per node because the
-// tie key is a bijection of the node index. Larger = better.
+// Candidate keys (pack_key / key_node, kp_device.hpp)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t pack_key(int32_t s, uint32_t tk) {
-  return (1ull << 63) | ((uint64_t)(uint32_t)s << 32) | (uint64_t)(~tk);
-}
-__device__ __forceinline__ int32_t key_node(uint64_t key, uint32_t sl, uint32_t inv) {
-  const uint32_t tk = ~(uint32_t)key;
-  return (int32_t)((tk - sl) * inv);
-}
 __device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
@@ -1129,13 +1105,13 @@ int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, in
 template <int D>
 struct RoundStartL {
   static int run(kp_ctx *c, int32_t lo, int32_t hi, int32_t *flag) {
-    const int32_t P = c->fits32 && c->N > 0 ? (c->N + 1023) & ~1023 : 0;
+    const int32_t P = !c->fits32 || c->N == 0 ? 0 : c->pack_fused ? c->fz_P : (c->N + 1023) & ~1023;
     const int64_t n = std::max<int64_t>(hi - lo, P);
     if (n <= 0) return KP_OK;
     hipLaunchKernelGGL((k_round_start<D>), dim3(blocks(n, 256)), dim3(256), 0, c->stream,
                        c->d.status, lo, hi, flag, c->d.cap, c->d.used, c->d.base, c->d.topo,
-                       c->pack_canonical ? c->d.perm : nullptr, c->N, P, c->pack_sp,
-                       c->d.np32);
+                       c->pack_canonical ? c->d.perm : nullptr,
+                       c->pack_fused ? c->d.colnode : nullptr, c->N, P, c->pack_sp, c->d.np32);
     KP_HIP(hipGetLastError());
     return KP_OK;
   }

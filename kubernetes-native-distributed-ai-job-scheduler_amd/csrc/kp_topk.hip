@@ -1,0 +1,446 @@
+// kp_topk.hip — gfx950 fused filter + score + top-K of the solve's candidate
+// phase: the J x N scores never reach HBM.
+//
+// The node table is packed in the class-aligned canonical layout (pack_node
+// with colnode: nodes sorted by capacity vector, every capacity class
+// starting on a 128-column wave tile, padding columns infeasible), so the 128
+// columns of a wave share one capacity vector and a pair's exact utilisation
+// is the compare-and-select form of k_score32's uniform path.
+//
+// k_score_topk: a 512-thread workgroup owns 1,024 columns (8 waves x 64 lanes
+// x 2 columns, tile operands in VGPRs) and streams its rows in chunks of 8:
+//   1. score — each wave computes the thresholds of its class for the
+//      chunk's rows (one exact division per (row, dim) lane), broadcasts them
+//      per row with v_readlane and writes its 128 scores of every row into a
+//      32-KB LDS tile;
+//   2. select — wave w reads row w of the chunk back (16 columns per lane):
+//      lane best of 32-bit truncated keys, bitonic sort of the 64 lane bests,
+//      T = the K-th of them (a lower bound of the tile's K-th key: K distinct
+//      columns reach it; truncation only keeps more), survivors >= T appended
+//      to LDS, exact ranks by counting; the tile's top-K exact keys, best
+//      first, go to part[row][tile]. More than 64 survivors (adversarial
+//      ties) switch to an exact bisection for the K-th 64-bit key.
+// k_merge_topk merges a row's per-tile lists into its K candidates, mapping
+// canonical position -> node through perm. Bit-exact with the materialised
+// path (k_score32 + k_select_t) and oracle kpo_round_candidates: every
+// global top-K key is in its tile's exact top-K.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "kp_device.hpp"
+#include "kp_internal.hpp"
+
+#ifndef KP_FZ_EXP
+#define KP_FZ_EXP 0
+#endif
+
+namespace kp {
+namespace {
+using namespace dev;
+
+constexpr int kFzWaves = 8;
+constexpr int kFzBS = 64 * kFzWaves;
+constexpr int kFzTile = 128 * kFzWaves;  // columns per workgroup (2 per lane)
+constexpr int kFzRC = 8;                 // rows per LDS chunk: one per wave in the select
+constexpr int kFzMaxRows = 128;          // rows per workgroup (request stage)
+constexpr int kFzSurv = 64;              // survivor slots per wave
+
+template <int D>
+constexpr int fz_dp() {
+  return D <= 1 ? 1 : D <= 2 ? 2 : D <= 4 ? 4 : 8;
+}
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, int lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+
+constexpr uint32_t kFzRowNoFit = 0x80000000u;  // WQ word flag: no column of the class fits
+
+template <int W>
+struct RowRec {  // one LDS row record in registers (W % 4 == 0 words)
+  uint4 v[W / 4];
+  __device__ __forceinline__ void load(const uint32_t *p) {
+#pragma unroll
+    for (int i = 0; i < W / 4; ++i) v[i] = reinterpret_cast<const uint4 *>(p)[i];
+  }
+  __device__ __forceinline__ uint32_t operator[](int j) const {
+    const uint4 &x = v[j >> 2];
+    return (j & 3) == 0 ? x.x : (j & 3) == 1 ? x.y : (j & 3) == 2 ? x.z : x.w;
+  }
+};
+
+// a wave-uniform value held in a VGPR (VOP3 compares / selects read at most
+// one scalar operand: the lane mask)
+__device__ __forceinline__ int32_t in_vgpr(int32_t x) {
+  int32_t r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
+  return r;
+}
+
+__device__ __forceinline__ int32_t comp(const int4 &v, int j) {
+  return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
+}
+
+template <int D, bool MOST>
+__global__ __launch_bounds__(kFzBS) void k_score_topk(
+    ScoreParams sp, const uint32_t *__restrict__ np, int32_t P, const int64_t *__restrict__ q,
+    int32_t qstride, const int32_t *__restrict__ uaff, const uint32_t *__restrict__ salt,
+    const int32_t *__restrict__ rows_unit, int32_t rows, int32_t rows_per_block, int32_t min_rpb,
+    const int32_t *__restrict__ rows_dev, const int32_t *__restrict__ wshift, int32_t ksh,
+    uint64_t *__restrict__ part) {
+  constexpr int DP = fz_dp<D>();  // lanes per row in the threshold stage
+  constexpr int SQW = D + 3;      // per row: requests, GPU request, affinity domain, tie salt
+  static_assert(kFzRC * DP <= 64, "threshold stage: one lane per (row, dim)");
+  __shared__ int4 ssc[kFzRC][kFzTile / 4];
+  __shared__ uint32_t sq[kFzMaxRows][SQW];
+  __shared__ uint64_t sbuf[kFzWaves][kFzSurv];
+  __shared__ uint32_t spos[kFzTile / 4];
+  constexpr int RW = (2 * D + 3 + 3) & ~3;  // row record words, whole 16-B reads
+  __shared__ __attribute__((aligned(16))) uint32_t srec[kFzWaves][kFzRC][RW];
+  if (rows_dev) fit_rows(*rows_dev, min_rpb, rows, rows_per_block);
+  const int r0 = blockIdx.y * rows_per_block;
+  if (r0 >= rows) return;  // block-uniform
+  const int nr = min(rows, r0 + rows_per_block) - r0;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntiles = gridDim.x, tile = blockIdx.x;
+  const int tile0 = tile * kFzTile;
+  const int g = sp.gpu_dim;
+  const int K = sp.n_cand;
+  for (int i = tid; i < nr * SQW; i += kFzBS) {
+    const int rr = i / SQW, d = i - rr * SQW;
+    const int32_t unit = rows_unit[r0 + rr];
+    uint32_t v;
+    if (d == D + 2) {
+      v = sp.tie_rotated ? salt[unit] : 0u;
+    } else if (d == D + 1) {
+      v = (uint32_t)uaff[unit];
+    } else {
+      const int dd = d < D ? d : g;
+      v = dd >= 0 ? (uint32_t)q[(int64_t)dd * qstride + unit] : 0u;
+    }
+    sq[rr][d] = v;
+  }
+  // the wave's 128 columns: 2 per lane, one 8-B load per plane
+  const uint2 *pv = reinterpret_cast<const uint2 *>(np);
+  const int64_t PV = P / 2, iv = (tile0 + wave * 128) / 2 + lane;
+  uint32_t f_[2][D], a_[2][D], fg_[2], tp_[2], cu[D];
+  int32_t b_[2], wa_[2];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const uint2 pf = pv[(kPlanes * d + 0) * PV + iv], pa = pv[(kPlanes * d + 2) * PV + iv];
+    f_[0][d] = pf.x;
+    f_[1][d] = pf.y;
+    a_[0][d] = pa.x;
+    a_[1][d] = pa.y;
+    // the class capacity: the wave's first column is always a node of its
+    // class (classes start on a wave tile); an all-padding wave reads 0
+    cu[d] = __builtin_amdgcn_readfirstlane(pv[(kPlanes * d + 1) * PV + iv].x);
+  }
+  {
+    const uint2 pb = pv[(kPlanes * D) * PV + iv], pt = pv[(kPlanes * D + 1) * PV + iv],
+                pw = pv[(kPlanes * D + 2) * PV + iv];
+    b_[0] = (int32_t)pb.x;
+    b_[1] = (int32_t)pb.y;
+    tp_[0] = pt.x;
+    tp_[1] = pt.y;
+    wa_[0] = (int32_t)pw.x;
+    wa_[1] = (int32_t)pw.y;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      fg_[k] = 0xFFFFFFFFu;  // no GPU dim: never equal to a request
+#pragma unroll
+      for (int d = 0; d < D; ++d)
+        if (d == g) fg_[k] = d == 0 ? f_[k][0] - 1u : f_[k][d];  // dim 0 holds free + 1
+    }
+  }
+  // select-phase column groups c = tile0 + 4*g (4 columns inside one wave
+  // tile): their canonical positions times the tie multiplier (padding
+  // columns get garbage, they are never feasible)
+  const uint32_t mul = sp.tie_rotated ? kTieMul : 1u;
+  if (tid < kFzTile / 4) {
+    const int c = tile0 + 4 * tid;
+    spos[tid] = (uint32_t)(c - wshift[c >> 7]) * mul;
+  }
+  __syncthreads();  // requests and positions staged
+  const uint32_t S = (uint32_t)sp.S;
+  int32_t wv[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) wv[d] = in_vgpr(sp.w[d]);
+  const int32_t wfitv = in_vgpr(sp.w_gpu_fit), waffv = in_vgpr(sp.w_affinity);
+  const int rsh = 32 - ksh;
+  for (int c0 = 0; c0 < nr; c0 += kFzRC) {
+    const int cr = min(kFzRC, nr - c0);
+    // 1a. the thresholds of this wave's class: lane -> (row lane/DP, dim
+    //     lane%DP), into the wave's LDS row records [q (dim 0: q + 1), GPU
+    //     request, affinity domain, thresholds, WQ | kRowNoFit]
+    {
+      const int rr = lane / DP, d = lane % DP;
+      uint32_t *rec = srec[wave][rr];
+      uint32_t tthr = 0xFFFFFFFFu, twq = 0, tok = 1u;
+      if (rr < cr && d < D) {
+        const uint32_t qd = sq[c0 + rr][d];
+        uint32_t c = 0, wd = 0;
+#pragma unroll
+        for (int dd = 0; dd < D; ++dd)
+          if (d == dd) {
+            c = cu[dd];
+            wd = (uint32_t)sp.w[dd];
+          }
+        if (c == 0u) {
+          tok = qd == 0u ? 1u : 0u;  // cap-0 dim: contributes 0, fits only q = 0
+        } else if (qd > c) {
+          tok = 0u;
+        } else {  // q*S = Q*c + rho: carry iff a >= c - rho
+          uint64_t Q, rho;
+          udivmod_uniform((uint64_t)qd * S, c, Q, rho);
+          tthr = c - (uint32_t)rho;
+          twq = wd * (uint32_t)Q;
+        }
+        rec[d] = qd + (d == 0 ? 1u : 0u);
+        rec[D + 2 + d] = tthr;
+      }
+#pragma unroll
+      for (int m = 1; m < DP; m <<= 1) {
+        twq += (uint32_t)__shfl_xor((int)twq, m, 64);
+        tok &= (uint32_t)__shfl_xor((int)tok, m, 64);
+      }
+      if (rr < cr && d == 0) {
+        rec[D] = sq[c0 + rr][D];
+        rec[D + 1] = sq[c0 + rr][D + 1];
+        rec[2 * D + 2] = tok ? twq : kFzRowNoFit;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // 1b. this wave's 128 scores of every row of the chunk -> LDS (the row
+    //     record is a broadcast read)
+    {
+#pragma unroll 1
+      for (int i = 0; i < cr; ++i) {
+        RowRec<RW> cur;
+        cur.load(srec[wave][i]);
+        const uint32_t wqw = cur[2 * D + 2], qg = cur[D], af = cur[D + 1];
+        const bool row_ok = !(wqw & kFzRowNoFit);
+        int32_t sv[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          bool ft = row_ok;
+          int32_t acc = wa_[k] + (int32_t)wqw + 1;  // s + 1
+#pragma unroll
+          for (int d = 0; d < D; ++d) {
+            ft &= cur[d] <= f_[k][d];
+            acc += a_[k][d] >= cur[D + 2 + d] ? wv[d] : 0;
+          }
+          // GPU-topology fit and the CacheStrategy=shared affinity bonus
+          const int32_t bonus =
+              ((qg != 0u && fg_[k] == qg) ? wfitv : 0) + (tp_[k] == af ? waffv : 0);
+          const int32_t sc = (MOST ? acc : b_[k] + 2 - acc) + bonus;
+          sv[k] = ft ? sc : 0;  // s + 1, 0 = infeasible
+        }
+        reinterpret_cast<int2 *>(ssc[i])[wave * 64 + lane] = make_int2(sv[0], sv[1]);
+      }
+    }
+    __syncthreads();  // the chunk's scores are in LDS
+    // 2. top-K of this tile for row `wave` of the chunk. LDS holds s + 1
+    //    (0 = infeasible); a column's 32-bit key is (s + 1) << ksh | the top
+    //    bits of ~tk, ~tk = ~(pos*mul + salt) = ~salt - pos*mul
+#if KP_FZ_EXP == 1  // timing experiment: no select phase
+    if (wave < cr && lane < K)  // no candidates (keeps the merge in bounds)
+      part[((r0 + c0 + wave) * ntiles + tile) * K + lane] = (uint64_t)(ssc[wave][lane].x & 0);
+    if (false)
+#endif
+    if (wave < cr) {
+      const int i = wave;
+      const int64_t row = r0 + c0 + i;
+      const uint32_t nsl = ~sq[c0 + i][D + 2];
+      uint32_t best = 0;
+#pragma unroll 1
+      for (int k = 0; k < 4; ++k) {
+        const int4 v = ssc[i][lane + 64 * k];
+        const uint32_t npk = nsl - spos[lane + 64 * k];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t s1 = (uint32_t)comp(v, j);
+          best = max(best, (s1 << ksh) | ((npk - (uint32_t)j * mul) >> rsh));
+        }
+      }
+      // T = the K-th largest lane best (radix select over ballots; lower
+      // bound of the tile's K-th key), at least 1 << ksh: every key >= T is
+      // feasible
+      uint32_t T = 0;
+#pragma unroll
+      for (int bb = 31; bb >= 0; --bb) {
+        const uint32_t cb = T | (1u << bb);
+        T = __popcll(__ballot(best >= cb)) >= K ? cb : T;
+      }
+      T = max(T, 1u << ksh);
+      // survivors (keys >= T) -> LDS as exact 64-bit keys, wave-compacted
+      asm volatile("" ::: "memory");  // re-read the row rather than hold it
+      int C = 0;
+#pragma unroll 1
+      for (int k = 0; k < 4; ++k) {
+        const int4 v = ssc[i][lane + 64 * k];
+        const uint32_t npk = nsl - spos[lane + 64 * k];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t s1 = (uint32_t)comp(v, j), ntk = npk - (uint32_t)j * mul;
+          const bool hit = ((s1 << ksh) | (ntk >> rsh)) >= T;
+          const uint64_t m = __ballot(hit);
+          if (m) {  // wave-uniform
+            const int p = C + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (hit && p < kFzSurv)
+              sbuf[wave][p] = ((uint64_t)(0x80000000u | (s1 - 1u)) << 32) | ntk;
+            C += __popcll(m);
+          }
+        }
+      }
+      if (C > kFzSurv) {
+        // exact K-th largest 64-bit key by bisection (> 64 keys reached T:
+        // adversarial ties; the columns are re-read from LDS)
+        const int32_t *srow = reinterpret_cast<const int32_t *>(ssc[i]);
+        uint64_t pre = 0;
+#pragma unroll 1
+        for (int bb = 63; bb >= 0; --bb) {
+          const uint64_t cb = pre | (1ull << bb);
+          int c = 0;
+#pragma unroll 1
+          for (int e = 0; e < 16; ++e) {
+            const int k = e >> 2, j = e & 3;
+            const uint32_t s1 = (uint32_t)srow[4 * (lane + 64 * k) + j];
+            const uint32_t ntk = nsl - spos[lane + 64 * k] - (uint32_t)j * mul;
+            c += (s1 != 0u && (((uint64_t)(0x80000000u | (s1 - 1u)) << 32) | ntk) >= cb) ? 1 : 0;
+          }
+          c = (int)rl((uint32_t)wave_incl_scan_i32(c), 63);
+          if (c >= K) pre = cb;
+        }
+        C = 0;
+#pragma unroll 1
+        for (int e = 0; e < 16; ++e) {
+          const int k = e >> 2, j = e & 3;
+          const uint32_t s1 = (uint32_t)srow[4 * (lane + 64 * k) + j];
+          const uint32_t ntk = nsl - spos[lane + 64 * k] - (uint32_t)j * mul;
+          const uint64_t key = ((uint64_t)(0x80000000u | (s1 - 1u)) << 32) | ntk;
+          const bool hit = s1 != 0u && key >= pre;
+          const uint64_t m = __ballot(hit);
+          const int p = C + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          if (hit) sbuf[wave][p] = key;
+          C += __popcll(m);  // = min(K, feasible) <= 32 in the end
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // exact rank of each survivor (one per lane; keys broadcast with
+      // v_readlane, no LDS round trip per step); ranks < K are the list
+      const uint64_t my = lane < C ? sbuf[wave][lane] : 0ull;
+      const uint32_t mlo = (uint32_t)my, mhi = (uint32_t)(my >> 32);
+      int r = 0;
+      for (int j = 0; j < C; ++j) {
+        const uint64_t o = ((uint64_t)rl(mhi, j) << 32) | rl(mlo, j);
+        r += o > my ? 1 : 0;
+      }
+      uint64_t *dst = part + (row * ntiles + tile) * K;
+      if (lane < C && r < K) dst[r] = my;
+      if (lane >= C && lane < K) dst[lane] = 0ull;
+    }
+    __syncthreads();  // the LDS tile is reused by the next chunk
+  }
+}
+
+// One wave per row: the row's ntiles sorted lists (ntiles * K keys, R per
+// lane), K times the wave max; keys are unique, so exactly one register of
+// one lane holds it and is cleared.
+template <int R>
+__global__ __launch_bounds__(256) void k_merge_topk(ScoreParams sp,
+                                                    const uint64_t *__restrict__ part,
+                                                    int32_t ntiles,
+                                                    const int32_t *__restrict__ rows_unit,
+                                                    const uint32_t *__restrict__ salt, int32_t rows,
+                                                    const int32_t *__restrict__ rows_dev,
+                                                    const int32_t *__restrict__ perm,
+                                                    int32_t *__restrict__ cand) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows || (rows_dev && row >= *rows_dev)) return;  // wave-uniform
+  const int K = sp.n_cand, M = ntiles * K;
+  const uint64_t *src = part + (int64_t)row * M;
+  uint64_t h[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int e = lane + 64 * r;
+    h[r] = e < M ? src[e] : 0ull;
+  }
+  const uint32_t sl = sp.tie_rotated ? salt[rows_unit[row]] : 0u;
+  const uint32_t inv = sp.tie_rotated ? kTieMulInv : 1u;
+  int32_t *out = cand + (int64_t)row * K;
+  for (int it = 0; it < K; ++it) {
+    uint64_t b = h[0];
+#pragma unroll
+    for (int r = 1; r < R; ++r) b = h[r] > b ? h[r] : b;
+    const uint64_t m = wave_max_u64_dpp(b);
+    if (m == 0) {  // fewer than K feasible nodes
+      if (lane >= it && lane < K) out[lane] = -1;
+      break;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (h[r] == m) h[r] = 0;
+    if (lane == 0) {  // canonical position -> node (a position is always < N)
+      const int32_t pos = key_node(m, sl, inv);
+      out[it] = (uint32_t)pos < (uint32_t)sp.N ? perm[pos] : -1;
+    }
+  }
+}
+
+template <int D>
+struct TopkL {
+  static int run(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
+                 int32_t ksh, int32_t *cand, const int32_t *rows_dev) {
+    const int P = c->fz_P, ntiles = P / kFzTile;
+    const int64_t want = ((int64_t)rows * ntiles + c->fz_wg_target - 1) / c->fz_wg_target;
+    const int rpb = (int)std::min<int64_t>(kFzMaxRows, std::max<int64_t>(kFzRC, want));
+    const dim3 grid(ntiles, blocks(rows, rpb));
+#define KP_FZ(M)                                                                                \
+  hipLaunchKernelGGL((k_score_topk<D, M>), grid, dim3(kFzBS), 0, c->stream, sp, c->d.np32, P, \
+                     c->d.q, c->U, c->d.aff, c->d.salt, rows_unit, rows, rpb, kFzRC, rows_dev,  \
+                     c->d.wshift, ksh, c->d.part)
+    if (sp.most_allocated)
+      KP_FZ(true);
+    else
+      KP_FZ(false);
+#undef KP_FZ
+    KP_HIP(hipGetLastError());
+    const int M = ntiles * sp.n_cand;
+    const dim3 mg(blocks(rows, 4));
+#define KP_MG(R)                                                                              \
+  hipLaunchKernelGGL((k_merge_topk<R>), mg, dim3(256), 0, c->stream, sp, c->d.part, ntiles, \
+                     rows_unit, c->d.salt, rows, rows_dev, c->d.perm, cand)
+    if (M <= 128)
+      KP_MG(2);
+    else if (M <= 256)
+      KP_MG(4);
+    else if (M <= 512)
+      KP_MG(8);
+    else if (M <= 1024)
+      KP_MG(16);
+    else
+      KP_MG(32);
+#undef KP_MG
+    KP_HIP(hipGetLastError());
+    return KP_OK;
+  }
+};
+
+}  // namespace
+
+int launch_score_topk(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
+                      int32_t ksh, int32_t *cand, const int32_t *rows_dev) {
+  if (rows <= 0 || c->N == 0) return KP_OK;
+  return dispatch_D<TopkL>(c->D, c, sp, rows_unit, rows, ksh, cand, rows_dev);
+}
+
+}  // namespace kp

@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-KP_ABI_VERSION = 2
+KP_ABI_VERSION = 3
 KP_MAX_DIMS = 8
 KP_MAX_CAND = 32
 KP_MAX_GANG = 64
@@ -94,7 +94,7 @@ class Timing(C.Structure):
         ("solve_ms", C.c_double), ("score_ms", C.c_double),
         ("select_ms", C.c_double), ("accept_ms", C.c_double),
         ("score_launches", C.c_int64), ("score_bytes", C.c_int64),
-        ("select_bytes", C.c_int64),
+        ("select_bytes", C.c_int64), ("fused", C.c_int32), ("reserved", C.c_int32),
     ]
 
 

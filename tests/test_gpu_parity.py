@@ -230,6 +230,92 @@ def test_active_compaction_paths_parity(oracle, monkeypatch, cmax):
     _assert_same(g, o, f"KP_COMPACT_MAX={cmax}")
 
 
+def few_class_workload(seed, J, N, D=4, classes=5, used_frac=0.5, affinity=True):
+    """Nodes of a few capacity classes (with cap-0 dims inside a class) and
+    random usage: the fused filter + score + top-K path's layout."""
+    rng = np.random.default_rng(seed)
+    shapes = rng.integers(1, 64, size=(classes, D)) * rng.choice([1, 7, 1000], size=(1, D))
+    shapes[rng.random((classes, D)) < 0.1] = 0
+    cap = np.ascontiguousarray(shapes[rng.integers(0, classes, size=N)].T.astype(np.int64))
+    used = (cap * rng.random((D, N)) * used_frac).astype(np.int64)
+    b = random_workload(seed, J, N, D=D)
+    aff = np.full(J, -1, np.int32)
+    if affinity:
+        for j in range(J):
+            same = j > 0 and b.gang_id[j] >= 0 and b.gang_id[j] == b.gang_id[j - 1]
+            aff[j] = aff[j - 1] if same else (rng.integers(0, N // 5) if rng.random() < 0.3 else -1)
+    return synth.Workload(J, N, D, b.req, cap, used, b.prio, b.gang_id, b.gang_size, b.topo,
+                          name=f"fc{seed}", affinity=aff)
+
+
+FUSED_CASES = [  # (D, score_mode, tie_mode, n_cand, N, classes)
+    (4, 0, 1, 16, 3000, 5), (1, 1, 0, 1, 700, 3), (2, 0, 0, 4, 1025, 2),
+    (3, 1, 1, 32, 2100, 9), (5, 0, 1, 8, 640, 4), (8, 1, 0, 16, 1500, 6),
+    (4, 1, 1, 5, 4100, 1), (4, 0, 0, 16, 130, 3),
+]
+
+
+@pytest.mark.parametrize("case", range(len(FUSED_CASES)))
+def test_fused_topk_parity(oracle, case):
+    """The fused filter + score + top-K candidate phase (no score matrix) is
+    bit-exact with the oracle: dims 1..8, both score modes and tie modes,
+    K in {1..32}, partial tiles, cap-0 dims inside classes, affinity."""
+    D, mode, tie, K, N, classes = FUSED_CASES[case]
+    w = few_class_workload(500 + case, J=2500, N=N, D=D, classes=classes)
+    p = _abi.default_params(score_mode=mode, tie_mode=tie, n_cand=K, gpu_dim=D - 1,
+                            w_dim=[(3 * d + 1) % 7 for d in range(8)], util_scale=[100, 7, 1024][case % 3])
+    with Placer(device=0) as pl:
+        g = pl.place(w, p)
+        assert pl.timing()["fused"] == 1
+    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
+    _assert_same(g, o, f"fused case {case}")
+
+
+@pytest.mark.parametrize("knobs", [
+    (("KP_FUSED", "0"),),           # materialised score matrix + select
+    (("KP_FZ_WG_TARGET", "64"),),   # 128 rows per fused workgroup
+    (("KP_FZ_WG_TARGET", "1000000"),),  # 8 rows (one chunk) per fused workgroup
+])
+def test_fused_knobs_parity(oracle, monkeypatch, knobs):
+    for k, v in knobs:
+        monkeypatch.setenv(k, v)
+    w = synth.config3(8_000, 1_300)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[3])
+    with Placer(device=0) as pl:
+        g = pl.place(w, p)
+        assert pl.timing()["fused"] == (0 if knobs[0] == ("KP_FUSED", "0") else 1)
+    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
+    _assert_same(g, o, f"fused knobs {knobs}")
+
+
+@pytest.mark.parametrize("tie", [0, 1])
+def test_fused_all_equal_nodes(oracle, tie):
+    """Identical empty nodes: every column of a tile ties on score, so the
+    32-bit keys cannot separate the survivors (tie_mode 0) and the exact
+    bisection path selects the tile's top-K."""
+    N, J = 3000, 400
+    cap = np.tile(np.array([[64000], [262144], [8], [1 << 20]], np.int64), (1, N))
+    w = synth.Workload(J, N, 4, np.tile(np.array([[1000], [4096], [1], [1 << 16]], np.int64), (1, J)),
+                       cap, np.zeros_like(cap), np.zeros(J, np.int32), np.full(J, -1, np.int32),
+                       np.ones(J, np.int32), (np.arange(N) // 8).astype(np.int32), name="equal")
+    p = _abi.default_params(tie_mode=tie)
+    with Placer(device=0) as pl:
+        g = pl.place(w, p)
+        assert pl.timing()["fused"] == 1
+    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
+    _assert_same(g, o, f"all equal tie {tie}")
+
+
+def test_fused_falls_back_on_many_classes(oracle, placer):
+    """Hundreds of capacity classes make the class-aligned layout too sparse:
+    the solve uses the materialised path, with the same result."""
+    w = random_workload(77, J=900, N=700)
+    p = _abi.default_params()
+    g, o = _place_both(oracle, placer, w, p)
+    assert placer.timing()["fused"] == 0
+    _assert_same(g, o, "many classes")
+
+
 def test_place_wide_rows_parity(oracle, placer):
     """Rows above 16384 nodes take the 1024-thread select form."""
     w = synth.config2(3_000, 20_000)
