@@ -1,20 +1,45 @@
-# Round evidence in one GPU call: full GPU test suite, the default bench line,
-# a rocprofv3 kernel-trace/stats profile of the bench command, and the
-# FETCH_SIZE / WRITE_SIZE PMC passes of the filter+score / select kernels.
+# Round evidence in one GPU call (outputs under gpurun_out/evidence; summarise
+# into profiles/ with tools/evidence_summary.py):
+#   1. the full GPU test suite (SKIP_TESTS=1 skips)
+#   2. the default bench line (SKIP_BENCH=1 skips)
+#   3. rocprofv3 --kernel-trace --stats of the config #3 solve steps
+#   4. the same for the config #4 (solve + preempt) and config #5 streaming legs
+#   5. PMC passes (one counter group each): FETCH_SIZE, WRITE_SIZE, the SQ
+#      issue/wait counters and the LDS bank-conflict counters of the hot kernels
+#   6. a HIP runtime trace of kp_place calls (hipMalloc / hipFree inside steps)
 set -o pipefail
 OUT=gpurun_out/evidence
-rm -rf $OUT; mkdir -p $OUT/prof $OUT/pmc
+rm -rf $OUT; mkdir -p $OUT/prof $OUT/prof45 $OUT/pmc $OUT/rt
 rocminfo 2>/dev/null | grep -m1 gfx950 > $OUT/arch.txt || true
-[ "$SKIP_TESTS" = 1 ] || timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
-[ "$SKIP_TESTS" = 1 ] || tail -1 $OUT/pytest_gpu.log
-[ "$SKIP_BENCH" = 1 ] || timeout -k 10 400 python -u bench.py --out $OUT/bench.json > $OUT/bench.log 2>&1 || exit $?
-echo bench ok
+if [ "$SKIP_TESTS" != 1 ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
+  tail -1 $OUT/pytest_gpu.log
+fi
+if [ "$SKIP_BENCH" != 1 ]; then
+  timeout -k 10 600 python -u bench.py --out $OUT/bench.json > $OUT/bench.log 2>&1 || { tail -20 $OUT/bench.log; exit 1; }
+  echo bench ok
+fi
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-stream --out $OUT/prof/bench_prof.json > $OUT/prof/bench.log 2>&1 || exit $?
+B3="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-stream --no-config4 --place-steps 0"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $B3 --out $OUT/prof/bench_prof.json > $OUT/prof/bench.log 2>&1 || exit $?
 echo prof ok
-for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 120 rocprofv3 --pmc $C --kernel-include-regex 'k_score|k_select' --output-format csv \
-    -d $OUT/pmc/$C -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-stream \
-    > $OUT/pmc/$C.log 2>&1 || exit $?
-  echo "$C ok"
-done
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof45 -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --place-steps 0 --c4-steps 1 --out $OUT/prof45/bench_prof.json > $OUT/prof45/bench.log 2>&1 || exit $?
+echo prof45 ok
+B1="bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-stream --no-config4 --place-steps 0"
+RE='k_score|k_select|k_merge|k_plan|k_accept'
+pmc() {  # name, counters...
+  local n=$1; shift
+  timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "$RE" --output-format csv \
+    -d $OUT/pmc/$n -o run -- python3 $B1 > $OUT/pmc/$n.log 2>&1 || return $?
+  echo "pmc $n ok"
+}
+pmc FETCH_SIZE FETCH_SIZE || exit $?
+pmc WRITE_SIZE WRITE_SIZE || exit $?
+pmc SQ1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY || exit $?
+pmc LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVES || exit $?
+timeout -k 10 300 rocprofv3 --hip-runtime-trace --kernel-trace --output-format csv -d $OUT/rt -o run -- python3 tools/place_steps.py > $OUT/rt/place.log 2>&1 || exit $?
+echo rt ok
+python3 tools/evidence_summary.py ${ROUND:-r02} $OUT $OUT/summary && ls $OUT/summary
+# the raw traces exceed what gpurun copies back: keep logs and summaries only
+rm -f $OUT/prof/run_kernel_trace.csv $OUT/prof45/run_kernel_trace.csv $OUT/*/*/run_counter_collection.csv $OUT/*/*/run_kernel_trace.csv
+du -sh $OUT
