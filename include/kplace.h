@@ -55,9 +55,12 @@ extern "C" {
 #define KP_SCORE_LEAST_ALLOCATED 1 /* spread  (kube-scheduler LeastAllocated) */
 
 /* ---- node tie-break modes ------------------------------------------------ */
-#define KP_TIE_NODE_INDEX 0 /* equal scores: lowest node index wins           */
-#define KP_TIE_ROTATED 1    /* equal scores: per-job Weyl rotation of the node
-                               index (deterministic stand-in for
+/* Both act on the node's canonical position pos(n): its rank when the nodes
+   are sorted by capacity vector (dim 0 first), then by index (DESIGN.md
+   §2.3). With one capacity vector for all nodes pos(n) = n. */
+#define KP_TIE_NODE_INDEX 0 /* equal scores: lowest canonical position wins    */
+#define KP_TIE_ROTATED 1    /* equal scores: per-job Weyl rotation of the
+                               canonical position (deterministic stand-in for
                                kube-scheduler's random selectHost)            */
 
 /* ---- score sentinels ---------------------------------------------------- */
