@@ -327,6 +327,7 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = std::getenv("KP_SCORE_NPL")) c->score_npl = std::atoi(e) == 4 ? 4 : 2;
   if (const char *e = std::getenv("KP_COMPACT_MAX")) c->compact_max = std::atoi(e);
   if (const char *e = std::getenv("KP_FUSED")) c->fused_enabled = std::atoi(e) != 0;
+  if (const char *e = std::getenv("KP_ACC_LIST")) c->acc_list = std::atoi(e);
   if (const char *e = std::getenv("KP_FZ_WG_TARGET")) c->fz_wg_target = std::max(64, std::atoi(e));
   if (hipSetDevice(dev) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -472,6 +473,7 @@ static int load_nodes_impl(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap,
   c->fz_layout_ok = fz_P > 0 && fz_cols - N <= N / 8 + 1024;
   c->fits32 = c->caps32 && c->reqs32 && c->jobs_loaded;
   c->util_scale_loaded = 0;  // force a division-table rebuild at the next solve
+  c->pack_full = true;
   c->nodes_loaded = true;
   return KP_OK;
 }
@@ -669,6 +671,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
                      c->max_cap < ((int64_t)1 << 31) && c->max_req < ((int64_t)1 << 31) &&
                      ksh >= 8 && (int64_t)(c->fz_P / 1024) * K <= 2048;
   c->pack_fused = fused;
+  c->pack_full = true;
   c->last_fused = fused;
   int64_t rpc = rows_per_chunk(c);
   if (fused) {
@@ -1170,6 +1173,7 @@ int kp_score(kp_ctx *c, const kp_params *p, int32_t job_lo, int32_t job_hi, int3
   c->pack_sp = sp;
   c->pack_canonical = false;  // kp_score returns columns in node order
   c->pack_fused = false;
+  c->pack_full = true;
   KP_TRY(launch_pack(c));  // 32-bit node planes of the current usage
   for (int64_t r0 = 0; r0 < rows; r0 += rpc) {
     const int32_t nr = (int32_t)std::min<int64_t>(rpc, rows - r0);

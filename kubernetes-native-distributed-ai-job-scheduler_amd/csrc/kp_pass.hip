@@ -29,6 +29,10 @@
 #include "kp_device.hpp"
 #include "kp_internal.hpp"
 
+#ifndef KP_ACC_FLAG_FIRST
+#define KP_ACC_FLAG_FIRST 0
+#endif
+
 namespace kp {
 namespace {
 using namespace dev;
@@ -467,6 +471,9 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
   const int N = ac.sp.N;
   const AcceptOut &o = ac.o;
   const int32_t nf = ac.node_flag[node];
+#if KP_ACC_FLAG_FIRST  // A/B: test the node flag before loading the node's operands
+  if (nf != pass) return;
+#endif
   const int32_t e0 = ac.seg_start[node];
   const int32_t e1 = ac.seg_end[node];
   int64_t rem[D], add[D];
@@ -634,8 +641,8 @@ struct AcceptL {
   static int run(kp_ctx *c, const ScoreParams &sp, int32_t pass, int64_t P) {
     const AccArgs ac = acc_args(c, sp, P);
     // rounds with fewer bidder entries than nodes walk the active-node list
-    const int32_t use_list = P < c->N ? 1 : 0;
-    const int64_t waves = use_list ? P : c->N;
+    const int32_t use_list = P < c->N || c->acc_list == 1 ? 1 : 0;
+    const int64_t waves = std::min<int64_t>(P, c->N);
     hipLaunchKernelGGL((k_accept<D>), dim3(blocks(waves, 4)), dim3(256), 0, c->stream, ac, pass,
                        use_list);
     KP_HIP(hipGetLastError());

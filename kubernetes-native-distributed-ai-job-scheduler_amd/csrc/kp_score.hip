@@ -145,55 +145,71 @@ __device__ __forceinline__ uint32_t mul_u24(uint32_t a, uint32_t b) {
 }
 
 
-// Round-start pack of the node table into the 32-bit form k_score32 consumes,
-// column i holding node perm[i] (the canonical order: nodes sorted by their
-// capacity vector; identity for kp_score). u32 SoA planes
-// [5*d + {0: free, 1: cap, 2: a, 3: R, 4: K}][P] where u*S (+ c - 1 for
-// LeastAllocated's ceiling) = A*c + a and (R, K) = div_prep(c), then the
+// Round-start pack of the node table into the 32-bit form k_score32 /
+// k_score_topk consume, column i holding node perm[i] (the canonical order:
+// nodes sorted by their capacity vector; identity for
+// kp_score) or colnode[i] (the fused solve's class-aligned layout). u32 SoA
+// planes [5*d + {0: free, 1: cap, 2: a, 3: R, 4: K}][P] where u*S (+ c - 1
+// for LeastAllocated's ceiling) = A*c + a and (R, K) = div_prep(c), then the
 // LeastAllocated base, the topo domain and WA = sum_d w_d*A_d in planes 5D,
-// 5D+1, 5D+2; P = round_up(N, 1024) (whole score tiles; padding columns are
-// zero and masked). One 8- or 16-B load per lane and plane fetches a lane's
-// consecutive columns.
-
+// 5D+1, 5D+2; padding columns are zero and masked. One 8- or 16-B load per
+// lane and plane fetches a lane's consecutive columns. The usage planes (free,
+// a, WA) change every round; the capacity planes (cap, R, K, base, topo) only
+// with the layout or the node table, so they are written when `full` is set.
+// A = floor(u*S / c) through the node's division table (R32, K32 of
+// k_prep_nodes: no 64-bit division per node and round).
 template <int D>
 __device__ __forceinline__ void pack_node(const int64_t *__restrict__ cap,
                                           const int64_t *__restrict__ used,
+                                          const uint32_t *__restrict__ R32,
+                                          const uint32_t *__restrict__ K32,
                                           const int64_t *__restrict__ base,
                                           const int32_t *__restrict__ topo,
                                           const int32_t *__restrict__ perm,
                                           const int32_t *__restrict__ colnode, int32_t N,
-                                          int32_t P, const ScoreParams &sp,
+                                          int32_t P, bool full, const ScoreParams &sp,
                                           uint32_t *__restrict__ np, int i) {
-  // colnode (the fused solve's class-aligned layout): column -> node, -1 =
-  // padding; the free plane of dim 0 then holds free + 1 (0 on padding), so
-  // that the fused kernel's fit test also rejects padding columns
+  // colnode: column -> node, -1 = padding; the free plane of dim 0 then holds
+  // free + 1 (0 on padding), so that the fused kernel's fit test also rejects
+  // padding columns
   const int cn = colnode ? colnode[i] : 0;
   const bool v = colnode ? cn >= 0 : i < N;
   const int n = !v ? 0 : colnode ? cn : perm ? perm[i] : i;
   const uint32_t plus1 = colnode && v ? 1u : 0u;
-  const uint64_t S = (uint64_t)sp.S;
+  const uint32_t S = (uint32_t)sp.S;
   uint32_t wa = 0;
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    const uint64_t cc = v ? (uint64_t)cap[(int64_t)d * N + n] : 0;
-    const uint64_t uu = v ? (uint64_t)used[(int64_t)d * N + n] : 0;
-    uint64_t A = 0, a = 0;
+    const int64_t j = (int64_t)d * N + n;
+    const uint32_t cc = v ? (uint32_t)cap[j] : 0u;
+    const uint32_t uu = v ? (uint32_t)used[j] : 0u;
+    const uint32_t R = v ? R32[j] : 0u, K = v ? K32[j] : (1u | kDivE);
+    uint32_t A = 0, a = 0;
     if (cc > 0) {
-      const uint64_t num = uu * S + (sp.most_allocated ? 0 : cc - 1);
-      A = num / cc;
-      a = num - A * cc;
+      bool nz;
+      const uint32_t t = div_floor32(uu, cc, R, K & 63u, S, nz);
+      const uint32_t r = (uint32_t)((uint64_t)uu * S - (uint64_t)t * cc);
+      if (sp.most_allocated) {
+        A = t;
+        a = r;
+      } else {  // (u*S + c - 1) = A*c + a
+        A = t + (nz ? 1u : 0u);
+        a = nz ? r - 1u : cc - 1u;
+      }
     }
-    uint32_t R = 0, K = 1u | kDivE;
-    div_prep(cc, (uint32_t)S, R, K);
-    wa += (uint32_t)sp.w[d] * (uint32_t)A;
-    np[(int64_t)(kPlanes * d + 0) * P + i] = (uint32_t)(cc - uu) + (d == 0 ? plus1 : 0u);
-    np[(int64_t)(kPlanes * d + 1) * P + i] = (uint32_t)cc;
-    np[(int64_t)(kPlanes * d + 2) * P + i] = (uint32_t)a;
-    np[(int64_t)(kPlanes * d + 3) * P + i] = R;
-    np[(int64_t)(kPlanes * d + 4) * P + i] = K;
+    wa += (uint32_t)sp.w[d] * A;
+    np[(int64_t)(kPlanes * d + 0) * P + i] = (cc - uu) + (d == 0 ? plus1 : 0u);
+    np[(int64_t)(kPlanes * d + 2) * P + i] = a;
+    if (full) {
+      np[(int64_t)(kPlanes * d + 1) * P + i] = cc;
+      np[(int64_t)(kPlanes * d + 3) * P + i] = R;
+      np[(int64_t)(kPlanes * d + 4) * P + i] = K;
+    }
   }
-  np[(int64_t)(kPlanes * D) * P + i] = v ? (uint32_t)base[n] : 0u;
-  np[(int64_t)(kPlanes * D + 1) * P + i] = v ? (uint32_t)topo[n] : 0xFFFFFFFFu;
+  if (full) {
+    np[(int64_t)(kPlanes * D) * P + i] = v ? (uint32_t)base[n] : 0u;
+    np[(int64_t)(kPlanes * D + 1) * P + i] = v ? (uint32_t)topo[n] : 0xFFFFFFFFu;
+  }
   np[(int64_t)(kPlanes * D + 2) * P + i] = wa;
 }
 
@@ -206,15 +222,18 @@ __global__ __launch_bounds__(256) void k_round_start(const int32_t *__restrict__
                                                      int32_t *__restrict__ flag,
                                                      const int64_t *__restrict__ cap,
                                                      const int64_t *__restrict__ used,
+                                                     const uint32_t *__restrict__ R32,
+                                                     const uint32_t *__restrict__ K32,
                                                      const int64_t *__restrict__ base,
                                                      const int32_t *__restrict__ topo,
                                                      const int32_t *__restrict__ perm,
                                                      const int32_t *__restrict__ colnode, int32_t N,
-                                                     int32_t P, ScoreParams sp,
+                                                     int32_t P, int32_t full, ScoreParams sp,
                                                      uint32_t *__restrict__ np) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < hi - lo) flag[i] = status[lo + i] == kActive ? 1 : 0;
-  if (i < P) pack_node<D>(cap, used, base, topo, perm, colnode, N, P, sp, np, i);
+  if (i < P)
+    pack_node<D>(cap, used, R32, K32, base, topo, perm, colnode, N, P, full != 0, sp, np, i);
 }
 
 // bit j of a 32-bit value -> bit 2j
@@ -1109,10 +1128,12 @@ struct RoundStartL {
     const int64_t n = std::max<int64_t>(hi - lo, P);
     if (n <= 0) return KP_OK;
     hipLaunchKernelGGL((k_round_start<D>), dim3(blocks(n, 256)), dim3(256), 0, c->stream,
-                       c->d.status, lo, hi, flag, c->d.cap, c->d.used, c->d.base, c->d.topo,
-                       c->pack_canonical ? c->d.perm : nullptr,
-                       c->pack_fused ? c->d.colnode : nullptr, c->N, P, c->pack_sp, c->d.np32);
+                       c->d.status, lo, hi, flag, c->d.cap, c->d.used, c->d.R32, c->d.K32,
+                       c->d.base, c->d.topo, c->pack_canonical ? c->d.perm : nullptr,
+                       c->pack_fused ? c->d.colnode : nullptr, c->N, P, c->pack_full ? 1 : 0,
+                       c->pack_sp, c->d.np32);
     KP_HIP(hipGetLastError());
+    if (P > 0) c->pack_full = false;  // capacity planes in place for this layout
     return KP_OK;
   }
 };

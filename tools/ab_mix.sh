@@ -1,0 +1,15 @@
+# A/B of library builds and environment knobs in ONE GPU call, alternated 3x:
+#   bash tools/ab_mix.sh a_base b_variant a_base@KP_ACC_LIST=1
+# each case = build/ab/<lib>.so [@VAR=VAL[,VAR=VAL]]; bench without events.
+set -o pipefail
+mkdir -p gpurun_out/ab
+AB=kubernetes-native-distributed-ai-job-scheduler_amd/build/ab
+for i in 1 2 3; do
+  for c in "$@"; do
+    lib=${c%%@*}; envs=""
+    [ "$c" != "$lib" ] && envs=$(echo "${c#*@}" | tr ',' ' ')
+    n=$(echo "$c" | tr '@=,' '___')
+    env $envs KPLACE_LIB=$PWD/$AB/$lib.so timeout -k 10 120 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-stream --no-config4 --place-steps 0 --no-kernel-events --out gpurun_out/ab/$n.$i.json > gpurun_out/ab/$n.$i.log 2>&1 || { tail -5 gpurun_out/ab/$n.$i.log; exit 1; }
+    python3 -c "import json;b=json.load(open('gpurun_out/ab/$n.$i.json'));print('$c', round(b['ms_per_step'],3), b['config']['rounds'], b['config']['passes'], b['config']['placed_jobs'])"
+  done
+done
