@@ -329,10 +329,13 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = std::getenv("KP_FUSED")) c->fused_enabled = std::atoi(e) != 0;
   if (const char *e = std::getenv("KP_ACC_LIST")) c->acc_list = std::atoi(e);
   if (const char *e = std::getenv("KP_FZ_WG_TARGET")) c->fz_wg_target = std::max(64, std::atoi(e));
+  if (const char *e = std::getenv("KP_COUNT_DIRECT")) c->count_direct = std::atoi(e) != 0;
   if (hipSetDevice(dev) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void **>(&c->pinned), 4096, hipHostMallocDefault) !=
           hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void **>(&c->pinned_coh), 64,
+                    hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
       hipMalloc(reinterpret_cast<void **>(&c->d.dl_bad), 16 * sizeof(int32_t)) != hipSuccess) {
     kp_destroy(c);
     return KP_EHIP;
@@ -753,12 +756,35 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     KP_TRY(E.make(&evA, hipEventDisableTiming));
     int32_t *A_h = c->pinned + 256;
     int64_t A_bound = shard;
+    // the round's count: stored by the compaction kernel into coherent pinned
+    // memory (spin on the -1 sentinel), or copied + event
+    auto round_count = [&](bool direct) -> int {
+      if (!direct) {
+        KP_HIP(hipEventSynchronize(evA));
+        return KP_OK;
+      }
+      const auto t0 = std::chrono::steady_clock::now();
+      int32_t v;
+      for (uint32_t spin = 0; (v = __atomic_load_n(c->pinned_coh, __ATOMIC_ACQUIRE)) < 0; ++spin) {
+        if ((spin & 1023u) == 1023u &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+          // not seen yet (e.g. a busy host): the stream has it for sure
+          KP_HIP(hipStreamSynchronize(c->stream));
+          v = __atomic_load_n(c->pinned_coh, __ATOMIC_ACQUIRE);
+          if (v < 0) return fail(KP_EHIP, "kp_solve: round count not delivered");
+          break;
+        }
+      }
+      *A_h = v;
+      return KP_OK;
+    };
     for (int32_t r = 0; A_bound > 0; ++r) {
       if (p->max_rounds > 0 && r >= p->max_rounds) break;
-      KP_TRY(launch_active_async(c, c->u_lo, c->u_hi, A_h));
-      KP_HIP(hipEventRecord(evA, c->stream));
+      bool direct = true;
+      KP_TRY(launch_active_async(c, c->u_lo, c->u_hi, A_h, &direct));
+      if (!direct) KP_HIP(hipEventRecord(evA, c->stream));
       if (A_bound > rpc) {  // chunked score matrix: needs the exact count first
-        KP_HIP(hipEventSynchronize(evA));
+        KP_TRY(round_count(direct));
         const int32_t A = *A_h;
         if (A == 0) break;
         for (int64_t r0 = 0; r0 < A; r0 += rpc)
@@ -771,7 +797,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
       const int32_t *A_dev = c->d.counters;
       KP_TRY(score_select(0, (int32_t)A_bound, A_dev, r));
       KP_TRY(passes_of_round((int32_t)A_bound, A_dev));
-      KP_HIP(hipEventSynchronize(evA));  // landed long ago on a busy round
+      KP_TRY(round_count(direct));  // landed long ago on a busy round
       round_active.push_back(*A_h);
       A_bound = *A_h;
     }
@@ -1000,6 +1026,7 @@ void kp_destroy(kp_ctx *c) {
     if (d.cand) (void)hipFree(d.cand);
   }
   if (c->pinned) (void)hipHostFree(c->pinned);
+  if (c->pinned_coh) (void)hipHostFree(c->pinned_coh);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }

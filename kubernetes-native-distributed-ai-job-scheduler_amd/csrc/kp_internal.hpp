@@ -185,6 +185,10 @@ struct kp_ctx {
   std::vector<int64_t> h_q;
   // pinned host scratch
   int32_t *pinned = nullptr;  // small counters
+  // coherent pinned word the compaction kernel stores the round's active
+  // count into (KP_COUNT_DIRECT=0: copy it with hipMemcpyAsync instead)
+  int32_t *pinned_coh = nullptr;
+  bool count_direct = true;
   kp::DevState d;
   // what the next node-plane pack builds: the solve's canonical column order
   // (scores by perm[column]) or kp_score's node order, for these params
@@ -222,7 +226,10 @@ int launch_score_topk(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit
 int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev = nullptr);
 int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass,
                 const int32_t *A_dev = nullptr);
-int launch_active_async(kp_ctx *c, int32_t lo, int32_t hi, int32_t *count_host);
+// direct (nullable): in, request the count stored by the compaction kernel
+// into c->pinned_coh (out: whether it was); else copied to count_host
+int launch_active_async(kp_ctx *c, int32_t lo, int32_t hi, int32_t *count_host,
+                        bool *direct = nullptr);
 int launch_accept(kp_ctx *c, const ScoreParams &sp, int32_t pass, int32_t A);
 int launch_active(kp_ctx *c, int32_t lo, int32_t hi, int32_t *A_host);
 int launch_reset_units(kp_ctx *c);

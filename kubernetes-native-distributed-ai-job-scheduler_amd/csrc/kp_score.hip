@@ -934,7 +934,8 @@ __global__ void k_delta_check(int32_t K, int32_t N, int32_t D, const int32_t *__
 constexpr int kCompactBS = 1024, kCompactIPT = 16;
 __global__ __launch_bounds__(kCompactBS) void k_compact(const int32_t *__restrict__ flag, int32_t n,
                                                         int32_t lo, int32_t *__restrict__ out,
-                                                        int32_t *__restrict__ count) {
+                                                        int32_t *__restrict__ count,
+                                                        int32_t *__restrict__ host_count) {
   __shared__ int32_t wsum[kCompactBS / kWave];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   int32_t carry = 0;
@@ -977,7 +978,12 @@ __global__ __launch_bounds__(kCompactBS) void k_compact(const int32_t *__restric
     carry += total;
     __syncthreads();  // wsum reused by the next chunk
   }
-  if (t == 0) *count = carry;
+  if (t == 0) {
+    *count = carry;
+    // the host's copy (pinned, coherent): a system-scope vector store, no
+    // copy command and no event in the stream
+    if (host_count) __hip_atomic_store(host_count, carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 template <int D>
@@ -1147,10 +1153,11 @@ int launch_pack(kp_ctx *c) { return launch_round_start(c, 0, 0, nullptr); }
 
 // flags[0, n) -> act_local (lo + index, rank order), count -> counters[0]; one
 // workgroup up to KP_COMPACT_MAX flags (default 262,144), rocprim::select above
-static int launch_compact(kp_ctx *c, const int32_t *flag, int32_t lo, int32_t n, size_t tb) {
+static int launch_compact(kp_ctx *c, const int32_t *flag, int32_t lo, int32_t n, size_t tb,
+                          int32_t *host_count = nullptr) {
   if (n <= c->compact_max) {
     hipLaunchKernelGGL(k_compact, dim3(1), dim3(kCompactBS), 0, c->stream, flag, n, lo,
-                       c->d.act_local, c->d.counters);
+                       c->d.act_local, c->d.counters, host_count);
     KP_HIP(hipGetLastError());
     return KP_OK;
   }
@@ -1200,11 +1207,20 @@ int launch_delta(kp_ctx *c, int32_t K, int32_t *bad_host) {
 // same compaction without the host round trip: the count stays on the device
 // (counters[0], read by the round's kernels) and is copied to *count_host
 // asynchronously
-int launch_active_async(kp_ctx *c, int32_t lo, int32_t hi, int32_t *count_host) {
+int launch_active_async(kp_ctx *c, int32_t lo, int32_t hi, int32_t *count_host, bool *direct) {
   const int32_t n = hi - lo;
   if (n <= 0) return KP_EINVAL;
   KP_TRY(launch_round_start(c, lo, hi, c->d.flag));
   size_t tb = c->d.temp_bytes;
+  // the one-workgroup compaction stores the count into coherent pinned
+  // memory itself (count_direct); otherwise a copy lands it
+  const bool dir = direct && c->count_direct && c->pinned_coh && n <= c->compact_max;
+  if (direct) *direct = dir;
+  if (dir) {
+    __atomic_store_n(c->pinned_coh, -1, __ATOMIC_RELAXED);  // the sentinel the host waits on
+    KP_TRY(launch_compact(c, c->d.flag, lo, n, tb, c->pinned_coh));
+    return KP_OK;
+  }
   KP_TRY(launch_compact(c, c->d.flag, lo, n, tb));
   KP_HIP(hipMemcpyAsync(count_host, c->d.counters, sizeof(int32_t), hipMemcpyDeviceToHost,
                         c->stream));

@@ -82,8 +82,15 @@ __device__ __forceinline__ int32_t comp(const int4 &v, int j) {
   return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
 }
 
+#ifndef KP_FZ_WAVES_PER_EU
+#define KP_FZ_WAVES_PER_EU 6  // 80 VGPRs: 3 workgroups of 8 waves per CU (a small spill is cheaper than 2)
+#endif
 template <int D, bool MOST>
-__global__ __launch_bounds__(kFzBS) void k_score_topk(
+__global__ __launch_bounds__(kFzBS)
+#if KP_FZ_WAVES_PER_EU
+__attribute__((amdgpu_waves_per_eu(KP_FZ_WAVES_PER_EU, KP_FZ_WAVES_PER_EU)))
+#endif
+void k_score_topk(
     ScoreParams sp, const uint32_t *__restrict__ np, int32_t P, const int64_t *__restrict__ q,
     int32_t qstride, const int32_t *__restrict__ uaff, const uint32_t *__restrict__ salt,
     const int32_t *__restrict__ rows_unit, int32_t rows, int32_t rows_per_block, int32_t min_rpb,
@@ -96,6 +103,7 @@ __global__ __launch_bounds__(kFzBS) void k_score_topk(
   __shared__ uint32_t sq[kFzMaxRows][SQW];
   __shared__ uint64_t sbuf[kFzWaves][kFzSurv];
   __shared__ uint32_t spos[kFzTile / 4];
+  __shared__ uint8_t scand[kFzWaves][64];  // per wave: lanes whose best reached T
   constexpr int RW = (2 * D + 3 + 3) & ~3;  // row record words, whole 16-B reads
   __shared__ __attribute__((aligned(16))) uint32_t srec[kFzWaves][kFzRC][RW];
   if (rows_dev) fit_rows(*rows_dev, min_rpb, rows, rows_per_block);
@@ -276,31 +284,40 @@ __global__ __launch_bounds__(kFzBS) void k_score_topk(
         T = __popcll(__ballot(best >= cb)) >= K ? cb : T;
       }
       T = max(T, 1u << ksh);
-      // survivors (keys >= T) -> LDS as exact 64-bit keys, wave-compacted
-      asm volatile("" ::: "memory");  // re-read the row rather than hold it
+      // survivors (keys >= T) -> LDS as exact 64-bit keys. Only lanes whose
+      // best reached T hold any (at least K of them): their lane numbers go
+      // to LDS in order and the whole wave scans just their 16 columns each
+      const uint64_t M = __ballot(best >= T);
+      const int m = __popcll(M);
+      if (best >= T)
+        scand[wave][__builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u))] =
+            (uint8_t)lane;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int32_t *srow = reinterpret_cast<const int32_t *>(ssc[i]);
       int C = 0;
-#pragma unroll 1
-      for (int k = 0; k < 4; ++k) {
-        const int4 v = ssc[i][lane + 64 * k];
-        const uint32_t npk = nsl - spos[lane + 64 * k];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t s1 = (uint32_t)comp(v, j), ntk = npk - (uint32_t)j * mul;
-          const bool hit = ((s1 << ksh) | (ntk >> rsh)) >= T;
-          const uint64_t m = __ballot(hit);
-          if (m) {  // wave-uniform
-            const int p = C + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            if (hit && p < kFzSurv)
-              sbuf[wave][p] = ((uint64_t)(0x80000000u | (s1 - 1u)) << 32) | ntk;
-            C += __popcll(m);
-          }
+      for (int e0 = 0; e0 < 16 * m; e0 += 64) {  // wave-uniform
+        const int e = e0 + lane;
+        bool hit = false;
+        uint32_t s1 = 0, ntk = 0;
+        if (e < 16 * m) {
+          const int L = scand[wave][e >> 4];          // candidate lane
+          const int g = L + 64 * ((e >> 2) & 3), jj = e & 3;  // its column group, column
+          s1 = (uint32_t)srow[4 * g + jj];
+          ntk = nsl - spos[g] - (uint32_t)jj * mul;
+          hit = ((s1 << ksh) | (ntk >> rsh)) >= T;
         }
+        const uint64_t mm = __ballot(hit);
+        const int p = C + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+        if (hit && p < kFzSurv) sbuf[wave][p] = ((uint64_t)(0x80000000u | (s1 - 1u)) << 32) | ntk;
+        C += __popcll(mm);
       }
       if (C > kFzSurv) {
         // exact K-th largest 64-bit key by bisection (> 64 keys reached T:
         // adversarial ties; the columns are re-read from LDS)
-        const int32_t *srow = reinterpret_cast<const int32_t *>(ssc[i]);
         uint64_t pre = 0;
 #pragma unroll 1
         for (int bb = 63; bb >= 0; --bb) {
