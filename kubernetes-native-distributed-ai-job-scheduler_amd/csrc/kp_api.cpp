@@ -330,6 +330,7 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = std::getenv("KP_ACC_LIST")) c->acc_list = std::atoi(e);
   if (const char *e = std::getenv("KP_FZ_WG_TARGET")) c->fz_wg_target = std::max(64, std::atoi(e));
   if (const char *e = std::getenv("KP_COUNT_DIRECT")) c->count_direct = std::atoi(e) != 0;
+  if (const char *e = std::getenv("KP_FZ_H16")) c->fz_h16 = std::atoi(e) != 0;
   if (hipSetDevice(dev) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void **>(&c->pinned), 4096, hipHostMallocDefault) !=

@@ -78,6 +78,32 @@ __device__ __forceinline__ int32_t in_vgpr(int32_t x) {
   return r;
 }
 
+// the 4 scores of 4-column group g of an LDS score row (u32 or packed u16)
+template <bool H16>
+__device__ __forceinline__ void load_group(const uint32_t *row, int g, uint32_t (&v)[4]) {
+  if constexpr (H16) {
+    const uint2 x = reinterpret_cast<const uint2 *>(row)[g];
+    v[0] = x.x & 0xFFFFu;
+    v[1] = x.x >> 16;
+    v[2] = x.y & 0xFFFFu;
+    v[3] = x.y >> 16;
+  } else {
+    const uint4 x = reinterpret_cast<const uint4 *>(row)[g];
+    v[0] = x.x;
+    v[1] = x.y;
+    v[2] = x.z;
+    v[3] = x.w;
+  }
+}
+
+template <bool H16>
+__device__ __forceinline__ uint32_t load_one(const uint32_t *row, int col) {
+  if constexpr (H16)
+    return reinterpret_cast<const uint16_t *>(row)[col];
+  else
+    return row[col];
+}
+
 __device__ __forceinline__ int32_t comp(const int4 &v, int j) {
   return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
 }
@@ -85,7 +111,7 @@ __device__ __forceinline__ int32_t comp(const int4 &v, int j) {
 #ifndef KP_FZ_WAVES_PER_EU
 #define KP_FZ_WAVES_PER_EU 6  // 80 VGPRs: 3 workgroups of 8 waves per CU (a small spill is cheaper than 2)
 #endif
-template <int D, bool MOST>
+template <int D, bool MOST, bool H16>
 __global__ __launch_bounds__(kFzBS)
 #if KP_FZ_WAVES_PER_EU
 __attribute__((amdgpu_waves_per_eu(KP_FZ_WAVES_PER_EU, KP_FZ_WAVES_PER_EU)))
@@ -99,7 +125,11 @@ void k_score_topk(
   constexpr int DP = fz_dp<D>();  // lanes per row in the threshold stage
   constexpr int SQW = D + 3;      // per row: requests, GPU request, affinity domain, tie salt
   static_assert(kFzRC * DP <= 64, "threshold stage: one lane per (row, dim)");
-  __shared__ int4 ssc[kFzRC][kFzTile / 4];
+  // the chunk's scores s + 1 (0 = infeasible): 16-bit and double-buffered
+  // (one barrier per chunk) when every score + 1 fits 16 bits, else 32-bit
+  // with a second barrier before the tile is rewritten
+  constexpr int NB = H16 ? 2 : 1, RWD = H16 ? kFzTile / 2 : kFzTile;  // buffers, words per row
+  __shared__ __attribute__((aligned(16))) uint32_t ssc[NB][kFzRC][RWD];
   __shared__ uint32_t sq[kFzMaxRows][SQW];
   __shared__ uint64_t sbuf[kFzWaves][kFzSurv];
   __shared__ uint32_t spos[kFzTile / 4];
@@ -179,6 +209,7 @@ void k_score_topk(
   const int rsh = 32 - ksh;
   for (int c0 = 0; c0 < nr; c0 += kFzRC) {
     const int cr = min(kFzRC, nr - c0);
+    const int buf = H16 ? (c0 / kFzRC) & 1 : 0;
     // 1a. the thresholds of this wave's class: lane -> (row lane/DP, dim
     //     lane%DP), into the wave's LDS row records [q (dim 0: q + 1), GPU
     //     request, affinity domain, thresholds, WQ | kRowNoFit]
@@ -247,7 +278,10 @@ void k_score_topk(
           const int32_t sc = (MOST ? acc : b_[k] + 2 - acc) + bonus;
           sv[k] = ft ? sc : 0;  // s + 1, 0 = infeasible
         }
-        reinterpret_cast<int2 *>(ssc[i])[wave * 64 + lane] = make_int2(sv[0], sv[1]);
+          if constexpr (H16)
+          ssc[buf][i][wave * 64 + lane] = (uint32_t)sv[0] | ((uint32_t)sv[1] << 16);
+        else
+          reinterpret_cast<int2 *>(ssc[0][i])[wave * 64 + lane] = make_int2(sv[0], sv[1]);
       }
     }
     __syncthreads();  // the chunk's scores are in LDS
@@ -256,7 +290,7 @@ void k_score_topk(
     //    bits of ~tk, ~tk = ~(pos*mul + salt) = ~salt - pos*mul
 #if KP_FZ_EXP == 1  // timing experiment: no select phase
     if (wave < cr && lane < K)  // no candidates (keeps the merge in bounds)
-      part[((r0 + c0 + wave) * ntiles + tile) * K + lane] = (uint64_t)(ssc[wave][lane].x & 0);
+      part[((r0 + c0 + wave) * ntiles + tile) * K + lane] = (uint64_t)(ssc[0][wave][lane] & 0);
     if (false)
 #endif
     if (wave < cr) {
@@ -266,11 +300,12 @@ void k_score_topk(
       uint32_t best = 0;
 #pragma unroll 1
       for (int k = 0; k < 4; ++k) {
-        const int4 v = ssc[i][lane + 64 * k];
+        uint32_t v4[4];
+        load_group<H16>(ssc[buf][i], lane + 64 * k, v4);
         const uint32_t npk = nsl - spos[lane + 64 * k];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const uint32_t s1 = (uint32_t)comp(v, j);
+          const uint32_t s1 = v4[j];
           best = max(best, (s1 << ksh) | ((npk - (uint32_t)j * mul) >> rsh));
         }
       }
@@ -296,7 +331,7 @@ void k_score_topk(
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const int32_t *srow = reinterpret_cast<const int32_t *>(ssc[i]);
+      const uint32_t *srow = ssc[buf][i];
       int C = 0;
       for (int e0 = 0; e0 < 16 * m; e0 += 64) {  // wave-uniform
         const int e = e0 + lane;
@@ -305,7 +340,7 @@ void k_score_topk(
         if (e < 16 * m) {
           const int L = scand[wave][e >> 4];          // candidate lane
           const int g = L + 64 * ((e >> 2) & 3), jj = e & 3;  // its column group, column
-          s1 = (uint32_t)srow[4 * g + jj];
+          s1 = load_one<H16>(srow, 4 * g + jj);
           ntk = nsl - spos[g] - (uint32_t)jj * mul;
           hit = ((s1 << ksh) | (ntk >> rsh)) >= T;
         }
@@ -326,7 +361,7 @@ void k_score_topk(
 #pragma unroll 1
           for (int e = 0; e < 16; ++e) {
             const int k = e >> 2, j = e & 3;
-            const uint32_t s1 = (uint32_t)srow[4 * (lane + 64 * k) + j];
+            const uint32_t s1 = load_one<H16>(srow, 4 * (lane + 64 * k) + j);
             const uint32_t ntk = nsl - spos[lane + 64 * k] - (uint32_t)j * mul;
             c += (s1 != 0u && (((uint64_t)(0x80000000u | (s1 - 1u)) << 32) | ntk) >= cb) ? 1 : 0;
           }
@@ -337,7 +372,7 @@ void k_score_topk(
 #pragma unroll 1
         for (int e = 0; e < 16; ++e) {
           const int k = e >> 2, j = e & 3;
-          const uint32_t s1 = (uint32_t)srow[4 * (lane + 64 * k) + j];
+          const uint32_t s1 = load_one<H16>(srow, 4 * (lane + 64 * k) + j);
           const uint32_t ntk = nsl - spos[lane + 64 * k] - (uint32_t)j * mul;
           const uint64_t key = ((uint64_t)(0x80000000u | (s1 - 1u)) << 32) | ntk;
           const bool hit = s1 != 0u && key >= pre;
@@ -364,7 +399,7 @@ void k_score_topk(
       if (lane < C && r < K) dst[r] = my;
       if (lane >= C && lane < K) dst[lane] = 0ull;
     }
-    __syncthreads();  // the LDS tile is reused by the next chunk
+    if constexpr (!H16) __syncthreads();  // the single LDS tile is rewritten next
   }
 }
 
@@ -421,14 +456,17 @@ struct TopkL {
     const int64_t want = ((int64_t)rows * ntiles + c->fz_wg_target - 1) / c->fz_wg_target;
     const int rpb = (int)std::min<int64_t>(kFzMaxRows, std::max<int64_t>(kFzRC, want));
     const dim3 grid(ntiles, blocks(rows, rpb));
-#define KP_FZ(M)                                                                                \
-  hipLaunchKernelGGL((k_score_topk<D, M>), grid, dim3(kFzBS), 0, c->stream, sp, c->d.np32, P, \
-                     c->d.q, c->U, c->d.aff, c->d.salt, rows_unit, rows, rpb, kFzRC, rows_dev,  \
+#define KP_FZ(M, H)                                                                              \
+  hipLaunchKernelGGL((k_score_topk<D, M, H>), grid, dim3(kFzBS), 0, c->stream, sp, c->d.np32, P, \
+                     c->d.q, c->U, c->d.aff, c->d.salt, rows_unit, rows, rpb, kFzRC, rows_dev,    \
                      c->d.wshift, ksh, c->d.part)
-    if (sp.most_allocated)
-      KP_FZ(true);
-    else
-      KP_FZ(false);
+    // 16-bit LDS scores when every score + 1 < 2^16 (ksh >= 16)
+    const bool h16 = ksh >= 16 && c->fz_h16;
+    if (sp.most_allocated) {
+      if (h16) KP_FZ(true, true); else KP_FZ(true, false);
+    } else {
+      if (h16) KP_FZ(false, true); else KP_FZ(false, false);
+    }
 #undef KP_FZ
     KP_HIP(hipGetLastError());
     const int M = ntiles * sp.n_cand;

@@ -275,6 +275,7 @@ def test_fused_topk_parity(oracle, case):
     (("KP_FUSED", "0"),),           # materialised score matrix + select
     (("KP_FZ_WG_TARGET", "64"),),   # 128 rows per fused workgroup
     (("KP_FZ_WG_TARGET", "1000000"),),  # 8 rows (one chunk) per fused workgroup
+    (("KP_FZ_H16", "0"),),          # 32-bit LDS scores (single buffer, two barriers)
 ])
 def test_fused_knobs_parity(oracle, monkeypatch, knobs):
     for k, v in knobs:
@@ -286,6 +287,20 @@ def test_fused_knobs_parity(oracle, monkeypatch, knobs):
         assert pl.timing()["fused"] == (0 if knobs[0] == ("KP_FUSED", "0") else 1)
     o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
     _assert_same(g, o, f"fused knobs {knobs}")
+
+
+@pytest.mark.parametrize("w,mode", [(1000, 0), (1000, 1), (40, 0)])
+def test_fused_wide_scores(oracle, w, mode):
+    """Scores above 2^16 take the fused kernel's 32-bit LDS form (w = 1000:
+    scores up to ~4e5, 13 tie-key bits in the 32-bit keys); w = 40 the 16-bit
+    form with scores up to ~1.6e4."""
+    wl = few_class_workload(900 + w + mode, J=2000, N=1500, D=4, classes=4)
+    p = _abi.default_params(score_mode=mode, w_dim=[w] * 8, w_gpu_fit=3 * w, w_affinity=w)
+    with Placer(device=0) as pl:
+        g = pl.place(wl, p)
+        assert pl.timing()["fused"] == 1
+    o = oracle.place(_snap(oracle, wl), p, nthreads=NTH)
+    _assert_same(g, o, f"wide scores w={w}")
 
 
 @pytest.mark.parametrize("tie", [0, 1])
