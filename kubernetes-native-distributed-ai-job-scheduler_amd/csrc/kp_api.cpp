@@ -661,8 +661,9 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   c->pack_canonical = true;  // the solve scores in canonical column order
   const int32_t shard = c->u_hi - c->u_lo;
   // Fused filter + score + top-K (kp_topk.hip) when the class-aligned layout
-  // is compact and every operand and score fits its 31-bit / 32-bit key
-  // field; else the materialised score matrix + top-K select.
+  // is compact, every cap and request < 2^30 (exact signed differences in its
+  // fit test) and every score fits the 32-bit key's score field; else the
+  // materialised score matrix + top-K select.
   int32_t ksh = 0;
   {
     int64_t bound = (int64_t)p->w_gpu_fit + p->w_affinity + 1;
@@ -672,7 +673,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     ksh = 32 - bits;  // (score + 1) << ksh keeps the score; >= 8 tie-key bits below it
   }
   const bool fused = c->fused_enabled && c->fz_layout_ok && c->fits32 &&
-                     c->max_cap < ((int64_t)1 << 31) && c->max_req < ((int64_t)1 << 31) &&
+                     c->max_cap < ((int64_t)1 << 30) && c->max_req < ((int64_t)1 << 30) &&
                      ksh >= 8 && (int64_t)(c->fz_P / 1024) * K <= 2048;
   c->pack_fused = fused;
   c->pack_full = true;

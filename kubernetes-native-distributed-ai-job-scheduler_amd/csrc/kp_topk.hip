@@ -55,8 +55,6 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, int lane) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
 }
 
-constexpr uint32_t kFzRowNoFit = 0x80000000u;  // WQ word flag: no column of the class fits
-
 template <int W>
 struct RowRec {  // one LDS row record in registers (W % 4 == 0 words)
   uint4 v[W / 4];
@@ -134,7 +132,7 @@ void k_score_topk(
   __shared__ uint64_t sbuf[kFzWaves][kFzSurv];
   __shared__ uint32_t spos[kFzTile / 4];
   __shared__ uint8_t scand[kFzWaves][64];  // per wave: lanes whose best reached T
-  constexpr int RW = (2 * D + 3 + 3) & ~3;  // row record words, whole 16-B reads
+  constexpr int RW = (2 * D + 4 + 3) & ~3;  // row record words, whole 16-B reads
   __shared__ __attribute__((aligned(16))) uint32_t srec[kFzWaves][kFzRC][RW];
   if (rows_dev) fit_rows(*rows_dev, min_rpb, rows, rows_per_block);
   const int r0 = blockIdx.y * rows_per_block;
@@ -205,14 +203,14 @@ void k_score_topk(
   int32_t wv[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) wv[d] = in_vgpr(sp.w[d]);
-  const int32_t wfitv = in_vgpr(sp.w_gpu_fit), waffv = in_vgpr(sp.w_affinity);
+  const int32_t waffv = in_vgpr(sp.w_affinity);
   const int rsh = 32 - ksh;
   for (int c0 = 0; c0 < nr; c0 += kFzRC) {
     const int cr = min(kFzRC, nr - c0);
     const int buf = H16 ? (c0 / kFzRC) & 1 : 0;
     // 1a. the thresholds of this wave's class: lane -> (row lane/DP, dim
     //     lane%DP), into the wave's LDS row records [q (dim 0: q + 1), GPU
-    //     request, affinity domain, thresholds, WQ | kRowNoFit]
+    //     request, affinity domain, thresholds, WQ, GPU-fit bonus]
     {
       const int rr = lane / DP, d = lane % DP;
       uint32_t *rec = srec[wave][rr];
@@ -236,7 +234,7 @@ void k_score_topk(
           tthr = c - (uint32_t)rho;
           twq = wd * (uint32_t)Q;
         }
-        rec[d] = qd + (d == 0 ? 1u : 0u);
+        if (d > 0) rec[d] = qd;
         rec[D + 2 + d] = tthr;
       }
 #pragma unroll
@@ -245,9 +243,14 @@ void k_score_topk(
         tok &= (uint32_t)__shfl_xor((int)tok, m, 64);
       }
       if (rr < cr && d == 0) {
-        rec[D] = sq[c0 + rr][D];
+        // dim 0 holds q + 1 against free + 1 (padding columns hold 0), or a
+        // request no column can meet when no column of the class fits
+        rec[0] = tok ? sq[c0 + rr][0] + 1u : 0x7FFFFFFFu;
+        const uint32_t qg = sq[c0 + rr][D];
+        rec[D] = qg;
         rec[D + 1] = sq[c0 + rr][D + 1];
-        rec[2 * D + 2] = tok ? twq : kFzRowNoFit;
+        rec[2 * D + 2] = twq;
+        rec[2 * D + 3] = qg != 0u ? (uint32_t)sp.w_gpu_fit : 0u;  // the row's GPU-fit bonus
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -260,23 +263,23 @@ void k_score_topk(
       for (int i = 0; i < cr; ++i) {
         RowRec<RW> cur;
         cur.load(srec[wave][i]);
-        const uint32_t wqw = cur[2 * D + 2], qg = cur[D], af = cur[D + 1];
-        const bool row_ok = !(wqw & kFzRowNoFit);
+        const uint32_t wq = cur[2 * D + 2], qg = cur[D], af = cur[D + 1];
+        const int32_t wfr = (int32_t)cur[2 * D + 3];
         int32_t sv[2];
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-          bool ft = row_ok;
-          int32_t acc = wa_[k] + (int32_t)wqw + 1;  // s + 1
+          // fit: every free - q >= 0; operands < 2^30, so the signed
+          // differences are exact and one min replaces D compares
+          int32_t mn = (int32_t)(f_[k][0] - cur[0]);
 #pragma unroll
-          for (int d = 0; d < D; ++d) {
-            ft &= cur[d] <= f_[k][d];
-            acc += a_[k][d] >= cur[D + 2 + d] ? wv[d] : 0;
-          }
+          for (int d = 1; d < D; ++d) mn = min(mn, (int32_t)(f_[k][d] - cur[d]));
+          int32_t acc = wa_[k] + (int32_t)wq + 1;  // s + 1
+#pragma unroll
+          for (int d = 0; d < D; ++d) acc += a_[k][d] >= cur[D + 2 + d] ? wv[d] : 0;
           // GPU-topology fit and the CacheStrategy=shared affinity bonus
-          const int32_t bonus =
-              ((qg != 0u && fg_[k] == qg) ? wfitv : 0) + (tp_[k] == af ? waffv : 0);
+          const int32_t bonus = (fg_[k] == qg ? wfr : 0) + (tp_[k] == af ? waffv : 0);
           const int32_t sc = (MOST ? acc : b_[k] + 2 - acc) + bonus;
-          sv[k] = ft ? sc : 0;  // s + 1, 0 = infeasible
+          sv[k] = mn >= 0 ? sc : 0;  // s + 1, 0 = infeasible
         }
           if constexpr (H16)
           ssc[buf][i][wave * 64 + lane] = (uint32_t)sv[0] | ((uint32_t)sv[1] << 16);
