@@ -48,6 +48,35 @@ __device__ __forceinline__ int64_t dpp_i64(int64_t v) {
   const uint32_t h2 = (uint32_t)__builtin_amdgcn_mov_dpp(hi, CTRL, 0xf, 0xf, false);
   return (int64_t)(((uint64_t)h2 << 32) | l2);
 }
+// 32-bit wave reductions (OP 0 = OR, 1 = AND, 2 = unsigned max), result in
+// every lane: DPP inside each 16-lane row, then the four row results through
+// scalar readlanes (VALU-only, no LDS crossbar)
+template <int OP>
+__device__ __forceinline__ uint32_t wave_red32_op(uint32_t a, uint32_t b) {
+  return OP == 0 ? (a | b) : OP == 1 ? (a & b) : (a > b ? a : b);
+}
+template <int OP>
+__device__ __forceinline__ uint32_t wave_red32(uint32_t v) {
+  const int rl16 = __lane_id() & 15;
+  uint32_t t;
+#define KP_STEP(CTRL, SH)                                                 \
+  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false); \
+  if (rl16 >= SH) v = wave_red32_op<OP>(v, t);
+  KP_STEP(0x111, 1)
+  KP_STEP(0x112, 2)
+  KP_STEP(0x114, 4)
+  KP_STEP(0x118, 8)
+#undef KP_STEP
+  uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+#pragma unroll
+  for (int r = 1; r < 4; ++r)
+    m = wave_red32_op<OP>(m, (uint32_t)__builtin_amdgcn_readlane((int)v, 16 * r + 15));
+  return m;
+}
+__device__ __forceinline__ uint32_t wave_or32(uint32_t v) { return wave_red32<0>(v); }
+__device__ __forceinline__ uint32_t wave_and32(uint32_t v) { return wave_red32<1>(v); }
+__device__ __forceinline__ uint32_t wave_max32(uint32_t v) { return wave_red32<2>(v); }
+
 // 64-bit wave max, result in every lane: DPP max inside each 16-lane row
 // (row_shr 1/2/4/8: lane 15 of a row ends with the row max), then the four
 // row maxima through scalar readlanes (VALU-only, no LDS crossbar)

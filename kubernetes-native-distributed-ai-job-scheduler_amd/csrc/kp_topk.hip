@@ -436,7 +436,11 @@ __global__ __launch_bounds__(256) void k_merge_topk(ScoreParams sp,
     uint64_t b = h[0];
 #pragma unroll
     for (int r = 1; r < R; ++r) b = h[r] > b ? h[r] : b;
-    const uint64_t m = wave_max_u64_dpp(b);
+    // 64-bit wave max as two 32-bit ones: the high words (valid bit |
+    // score), then the low words (~tie key) among the lanes holding that max
+    const uint32_t mhi = wave_max32((uint32_t)(b >> 32));
+    const uint32_t mlo = wave_max32((uint32_t)(b >> 32) == mhi ? (uint32_t)b : 0u);
+    const uint64_t m = ((uint64_t)mhi << 32) | mlo;
     if (m == 0) {  // fewer than K feasible nodes
       if (lane >= it && lane < K) out[lane] = -1;
       break;
