@@ -45,6 +45,8 @@ def _worker(rank, world, port, cfg, mpm, out_q):
         return b"".join(b.numpy().tobytes() for b in bufs)
 
     no, J, N = cfg
+    if mpm:  # the chunked matrix belongs to the materialised candidate phase
+        os.environ["KP_FUSED"] = "0"
     w = synth.config(no, J, N)
     p = _abi.default_params(**synth.CONFIG_PARAMS[no])
     with Placer(device=0, world_size=world, rank=rank, allgather=allgather,

@@ -303,6 +303,20 @@ def test_fused_wide_scores(oracle, w, mode):
     _assert_same(g, o, f"wide scores w={w}")
 
 
+@pytest.mark.parametrize("mpm", [512 * 900, 640 * 3000])
+def test_materialised_chunked_parity(oracle, monkeypatch, mpm):
+    """The materialised candidate phase with a score matrix chunked into
+    several row blocks per round (the exact-count round path)."""
+    monkeypatch.setenv("KP_FUSED", "0")
+    w = synth.config3(9_000, 640)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[3])
+    with Placer(device=0, max_pairs_matrix=mpm) as pl:
+        g = pl.place(w, p)
+        assert pl.timing()["fused"] == 0
+    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
+    _assert_same(g, o, f"chunked mpm={mpm}")
+
+
 @pytest.mark.parametrize("tie", [0, 1])
 def test_fused_all_equal_nodes(oracle, tie):
     """Identical empty nodes: every column of a tile ties on score, so the
