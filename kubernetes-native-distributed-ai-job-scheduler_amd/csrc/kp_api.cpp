@@ -331,6 +331,9 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = std::getenv("KP_FZ_WG_TARGET")) c->fz_wg_target = std::max(64, std::atoi(e));
   if (const char *e = std::getenv("KP_COUNT_DIRECT")) c->count_direct = std::atoi(e) != 0;
   if (const char *e = std::getenv("KP_FZ_H16")) c->fz_h16 = std::atoi(e) != 0;
+  if (const char *e = std::getenv("KP_FZ_PROF"))  // phase clocks (KP_FZ_PROFILE builds only)
+    if (std::atoi(e) != 0 && hipMalloc(reinterpret_cast<void **>(&c->d.fz_prof), 16 * 8) == hipSuccess)
+      (void)hipMemset(c->d.fz_prof, 0, 16 * 8);
   if (hipSetDevice(dev) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void **>(&c->pinned), 4096, hipHostMallocDefault) !=
@@ -1010,6 +1013,14 @@ void kp_destroy(kp_ctx *c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->nccl_comm) ncclCommDestroy(static_cast<ncclComm_t>(c->nccl_comm));
   DevState &d = c->d;
+  if (d.fz_prof) {  // KP_FZ_PROF: the accumulated phase clocks
+    uint64_t h[16] = {0};
+    if (hipMemcpy(h, d.fz_prof, sizeof h, hipMemcpyDeviceToHost) == hipSuccess) {
+      std::fprintf(stderr, "kp_fz_prof");
+      for (int i = 0; i < 9; ++i) std::fprintf(stderr, " %llu", (unsigned long long)h[i]);
+      std::fprintf(stderr, "\n");
+    }
+  }
   void *ptrs[] = {d.cap, d.used, d.used0, d.R32, d.K32, d.base, d.topo, d.q, d.leader, d.size,
                   d.status, d.salt, d.aff,
                   d.job_node, d.job_score, d.job_status, d.act_local, d.cand_local, d.score,
@@ -1020,7 +1031,7 @@ void kp_destroy(kp_ctx *c) {
                   d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
                   d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.roff,
                   d.rreq, d.rsuf, d.rprio, d.pre_node, d.pre_vict, d.pre_cost,
-                  d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.stats, d.np32, d.colnode, d.wshift, d.part};
+                  d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.stats, d.np32, d.colnode, d.wshift, d.part, d.fz_prof};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->world > 1) {

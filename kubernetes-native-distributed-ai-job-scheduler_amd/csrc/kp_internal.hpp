@@ -65,6 +65,7 @@ struct DevState {
   int32_t *colnode = nullptr;  // [fz_P]
   int32_t *wshift = nullptr;   // [fz_P / 128]
   uint64_t *part = nullptr;    // [rows][fz_P / 1024][K] per-tile top-K keys
+  uint64_t *fz_prof = nullptr; // [16] phase clocks of a KP_FZ_PROFILE build (KP_FZ_PROF=1)
   // units (rank order), job outputs
   int64_t *q = nullptr;  // [D][U]
   int32_t *leader = nullptr, *size = nullptr, *status = nullptr;

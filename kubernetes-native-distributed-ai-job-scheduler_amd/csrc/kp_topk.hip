@@ -34,6 +34,32 @@
 #ifndef KP_FZ_EXP
 #define KP_FZ_EXP 0
 #endif
+// KP_FZ_PROFILE: per-phase shader-clock sums (s_memtime deltas of every
+// wave, lane 0 adds them into prof[phase]); a timing build only
+#ifdef KP_FZ_PROFILE
+#define KP_FZ_PROF_MARK(ph)                           \
+  do {                                                \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime(); \
+    pacc_[ph] += now_ - t_prev_;                      \
+    t_prev_ = now_;                                   \
+  } while (0)
+#define KP_FZ_PROF_FLUSH()                                                               \
+  do {                                                                                   \
+    if (prof && lane == 0)                                                               \
+      for (int p_ = 0; p_ < 9; ++p_)                                                     \
+        atomicAdd((unsigned long long *)&prof[p_], (unsigned long long)pacc_[p_]);       \
+  } while (0)
+#else
+#define KP_FZ_PROF_MARK(ph) \
+  do {                      \
+  } while (0)
+#define KP_FZ_PROF_FLUSH() \
+  do {                     \
+  } while (0)
+#endif
+#ifndef KP_FZ_ROW_UNROLL
+#define KP_FZ_ROW_UNROLL 1  // rows of the score loop interleaved (A/B knob)
+#endif
 
 namespace kp {
 namespace {
@@ -53,6 +79,22 @@ constexpr int fz_dp() {
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, int lane) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+
+// value of lane ^ M (M = 1, 2, 4) through DPP: quad permutes for 1 and 2,
+// row shifts by 4 for 4 (VALU only, no LDS crossbar)
+template <int M>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
+  if constexpr (M == 1) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);  // [1,0,3,2]
+  } else if constexpr (M == 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);  // [2,3,0,1]
+  } else {
+    static_assert(M == 4, "xor 1, 2 or 4");
+    const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x104, 0xf, 0xf, false);  // row_shl:4
+    const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    return (__lane_id() & 4) ? dn : up;
+  }
 }
 
 template <int W>
@@ -102,9 +144,6 @@ __device__ __forceinline__ uint32_t load_one(const uint32_t *row, int col) {
     return row[col];
 }
 
-__device__ __forceinline__ int32_t comp(const int4 &v, int j) {
-  return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
-}
 
 #ifndef KP_FZ_WAVES_PER_EU
 #define KP_FZ_WAVES_PER_EU 6  // 80 VGPRs: 3 workgroups of 8 waves per CU (a small spill is cheaper than 2)
@@ -119,7 +158,7 @@ void k_score_topk(
     int32_t qstride, const int32_t *__restrict__ uaff, const uint32_t *__restrict__ salt,
     const int32_t *__restrict__ rows_unit, int32_t rows, int32_t rows_per_block, int32_t min_rpb,
     const int32_t *__restrict__ rows_dev, const int32_t *__restrict__ wshift, int32_t ksh,
-    uint64_t *__restrict__ part) {
+    uint64_t *__restrict__ part, uint64_t *__restrict__ prof) {
   constexpr int DP = fz_dp<D>();  // lanes per row in the threshold stage
   constexpr int SQW = D + 3;      // per row: requests, GPU request, affinity domain, tie salt
   static_assert(kFzRC * DP <= 64, "threshold stage: one lane per (row, dim)");
@@ -140,6 +179,11 @@ void k_score_topk(
   const int nr = min(rows, r0 + rows_per_block) - r0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntiles = gridDim.x, tile = blockIdx.x;
+#ifdef KP_FZ_PROFILE
+  uint64_t t_prev_ = __builtin_amdgcn_s_memtime(), pacc_[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#else
+  (void)prof;
+#endif
   const int tile0 = tile * kFzTile;
   const int g = sp.gpu_dim;
   const int K = sp.n_cand;
@@ -160,7 +204,7 @@ void k_score_topk(
   // the wave's 128 columns: 2 per lane, one 8-B load per plane
   const uint2 *pv = reinterpret_cast<const uint2 *>(np);
   const int64_t PV = P / 2, iv = (tile0 + wave * 128) / 2 + lane;
-  uint32_t f_[2][D], a_[2][D], fg_[2], tp_[2], cu[D];
+  uint32_t f_[2][D], a_[2][D], fg_[2], tp_[2], cu[D], cR[D], cK[D];
   int32_t b_[2], wa_[2];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
@@ -172,6 +216,8 @@ void k_score_topk(
     // the class capacity: the wave's first column is always a node of its
     // class (classes start on a wave tile); an all-padding wave reads 0
     cu[d] = __builtin_amdgcn_readfirstlane(pv[(kPlanes * d + 1) * PV + iv].x);
+    cR[d] = __builtin_amdgcn_readfirstlane(pv[(kPlanes * d + 3) * PV + iv].x);
+    cK[d] = __builtin_amdgcn_readfirstlane(pv[(kPlanes * d + 4) * PV + iv].x);
   }
   {
     const uint2 pb = pv[(kPlanes * D) * PV + iv], pt = pv[(kPlanes * D + 1) * PV + iv],
@@ -198,7 +244,9 @@ void k_score_topk(
     const int c = tile0 + 4 * tid;
     spos[tid] = (uint32_t)(c - wshift[c >> 7]) * mul;
   }
+  KP_FZ_PROF_MARK(0);
   __syncthreads();  // requests and positions staged
+  KP_FZ_PROF_MARK(1);
   const uint32_t S = (uint32_t)sp.S;
   int32_t wv[D];
 #pragma unroll
@@ -228,19 +276,34 @@ void k_score_topk(
           tok = qd == 0u ? 1u : 0u;  // cap-0 dim: contributes 0, fits only q = 0
         } else if (qd > c) {
           tok = 0u;
-        } else {  // q*S = Q*c + rho: carry iff a >= c - rho
-          uint64_t Q, rho;
-          udivmod_uniform((uint64_t)qd * S, c, Q, rho);
-          tthr = c - (uint32_t)rho;
-          twq = wd * (uint32_t)Q;
+        } else {  // q*S = Q*c + rho: carry iff a >= c - rho (the class's division table)
+          uint32_t R = 0, Kd = 0;
+#pragma unroll
+          for (int dd = 0; dd < D; ++dd)
+            if (d == dd) {
+              R = cR[dd];
+              Kd = cK[dd];
+            }
+          bool nz;
+          const uint32_t Q = div_floor32(qd, c, R, Kd, S, nz);
+          const uint32_t rho = (uint32_t)((uint64_t)qd * S - (uint64_t)Q * c);
+          tthr = c - rho;
+          twq = wd * Q;
         }
         if (d > 0) rec[d] = qd;
         rec[D + 2 + d] = tthr;
       }
-#pragma unroll
-      for (int m = 1; m < DP; m <<= 1) {
-        twq += (uint32_t)__shfl_xor((int)twq, m, 64);
-        tok &= (uint32_t)__shfl_xor((int)tok, m, 64);
+      if constexpr (DP >= 2) {
+        twq += lane_xor<1>(twq);
+        tok &= lane_xor<1>(tok);
+      }
+      if constexpr (DP >= 4) {
+        twq += lane_xor<2>(twq);
+        tok &= lane_xor<2>(tok);
+      }
+      if constexpr (DP >= 8) {
+        twq += lane_xor<4>(twq);
+        tok &= lane_xor<4>(tok);
       }
       if (rr < cr && d == 0) {
         // dim 0 holds q + 1 against free + 1 (padding columns hold 0), or a
@@ -256,10 +319,15 @@ void k_score_topk(
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    KP_FZ_PROF_MARK(2);
     // 1b. this wave's 128 scores of every row of the chunk -> LDS (the row
     //     record is a broadcast read)
     {
+#if KP_FZ_ROW_UNROLL == 2
+#pragma unroll 2
+#else
 #pragma unroll 1
+#endif
       for (int i = 0; i < cr; ++i) {
         RowRec<RW> cur;
         cur.load(srec[wave][i]);
@@ -287,7 +355,9 @@ void k_score_topk(
           reinterpret_cast<int2 *>(ssc[0][i])[wave * 64 + lane] = make_int2(sv[0], sv[1]);
       }
     }
+    KP_FZ_PROF_MARK(3);
     __syncthreads();  // the chunk's scores are in LDS
+    KP_FZ_PROF_MARK(4);
     // 2. top-K of this tile for row `wave` of the chunk. LDS holds s + 1
     //    (0 = infeasible); a column's 32-bit key is (s + 1) << ksh | the top
     //    bits of ~tk, ~tk = ~(pos*mul + salt) = ~salt - pos*mul
@@ -315,6 +385,7 @@ void k_score_topk(
       // T = the K-th largest lane best (radix select over ballots; lower
       // bound of the tile's K-th key), at least 1 << ksh: every key >= T is
       // feasible
+      KP_FZ_PROF_MARK(5);
       uint32_t T = 0;
 #pragma unroll
       for (int bb = 31; bb >= 0; --bb) {
@@ -325,6 +396,7 @@ void k_score_topk(
       // survivors (keys >= T) -> LDS as exact 64-bit keys. Only lanes whose
       // best reached T hold any (at least K of them): their lane numbers go
       // to LDS in order and the whole wave scans just their 16 columns each
+      KP_FZ_PROF_MARK(6);
       const uint64_t M = __ballot(best >= T);
       const int m = __popcll(M);
       if (best >= T)
@@ -389,6 +461,7 @@ void k_score_topk(
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      KP_FZ_PROF_MARK(7);
       // exact rank of each survivor (one per lane; keys broadcast with
       // v_readlane, no LDS round trip per step); ranks < K are the list
       const uint64_t my = lane < C ? sbuf[wave][lane] : 0ull;
@@ -402,8 +475,10 @@ void k_score_topk(
       if (lane < C && r < K) dst[r] = my;
       if (lane >= C && lane < K) dst[lane] = 0ull;
     }
+    KP_FZ_PROF_MARK(8);
     if constexpr (!H16) __syncthreads();  // the single LDS tile is rewritten next
   }
+  KP_FZ_PROF_FLUSH();
 }
 
 // One wave per row: the row's ntiles sorted lists (ntiles * K keys, R per
@@ -466,7 +541,7 @@ struct TopkL {
 #define KP_FZ(M, H)                                                                              \
   hipLaunchKernelGGL((k_score_topk<D, M, H>), grid, dim3(kFzBS), 0, c->stream, sp, c->d.np32, P, \
                      c->d.q, c->U, c->d.aff, c->d.salt, rows_unit, rows, rpb, kFzRC, rows_dev,    \
-                     c->d.wshift, ksh, c->d.part)
+                     c->d.wshift, ksh, c->d.part, c->d.fz_prof)
     // 16-bit LDS scores when every score + 1 < 2^16 (ksh >= 16)
     const bool h16 = ksh >= 16 && c->fz_h16;
     if (sp.most_allocated) {
