@@ -20,7 +20,7 @@
 //      to LDS, exact ranks by counting; the tile's top-K exact keys, best
 //      first, go to part[row][tile]. More than 64 survivors (adversarial
 //      ties) switch to an exact bisection for the K-th 64-bit key.
-// k_merge_topk merges a row's per-tile lists into its K candidates, mapping
+// k_merge_tour merges a row's per-tile lists into its K candidates, mapping
 // canonical position -> node through perm. Bit-exact with the materialised
 // path (k_score32 + k_select_t) and oracle kpo_round_candidates: every
 // global top-K key is in its tile's exact top-K.
@@ -481,38 +481,45 @@ void k_score_topk(
   KP_FZ_PROF_FLUSH();
 }
 
-// One wave per row: the row's ntiles sorted lists (ntiles * K keys, R per
-// lane), K times the wave max; keys are unique, so exactly one register of
-// one lane holds it and is cleared.
-template <int R>
-__global__ __launch_bounds__(256) void k_merge_topk(ScoreParams sp,
-                                                    const uint64_t *__restrict__ part,
+// Tournament form: the row's ntiles sorted lists are staged in LDS, lane t
+// holds the heads of lists t, t+64, ... (LPL per lane); K times the wave
+// max of the heads, and only the owner of the max advances its list (one LDS
+// read). K x (one wave max + one LDS read) per row instead of K passes over
+// all ntiles*K keys. Dynamic LDS: 4 rows x ntiles*K keys.
+template <int LPL>
+__global__ __launch_bounds__(256) void k_merge_tour(ScoreParams sp, const uint64_t *__restrict__ part,
                                                     int32_t ntiles,
                                                     const int32_t *__restrict__ rows_unit,
                                                     const uint32_t *__restrict__ salt, int32_t rows,
                                                     const int32_t *__restrict__ rows_dev,
                                                     const int32_t *__restrict__ perm,
                                                     int32_t *__restrict__ cand) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows || (rows_dev && row >= *rows_dev)) return;  // wave-uniform
+  extern __shared__ uint64_t slist[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row = blockIdx.x * 4 + wave;
+  if (row >= rows || (rows_dev && row >= *rows_dev)) return;  // wave-uniform, no barrier below
   const int K = sp.n_cand, M = ntiles * K;
+  uint64_t *L = slist + (int64_t)wave * M;
   const uint64_t *src = part + (int64_t)row * M;
-  uint64_t h[R];
+  for (int e = lane; e < M; e += 64) L[e] = src[e];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  int h[LPL];
+  uint64_t v[LPL];
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int e = lane + 64 * r;
-    h[r] = e < M ? src[e] : 0ull;
+  for (int j = 0; j < LPL; ++j) {
+    const int t = lane + 64 * j;
+    h[j] = 0;
+    v[j] = t < ntiles ? L[t * K] : 0ull;
   }
   const uint32_t sl = sp.tie_rotated ? salt[rows_unit[row]] : 0u;
   const uint32_t inv = sp.tie_rotated ? kTieMulInv : 1u;
   int32_t *out = cand + (int64_t)row * K;
   for (int it = 0; it < K; ++it) {
-    uint64_t b = h[0];
+    uint64_t b = v[0];
 #pragma unroll
-    for (int r = 1; r < R; ++r) b = h[r] > b ? h[r] : b;
-    // 64-bit wave max as two 32-bit ones: the high words (valid bit |
-    // score), then the low words (~tie key) among the lanes holding that max
+    for (int j = 1; j < LPL; ++j) b = v[j] > b ? v[j] : b;
     const uint32_t mhi = wave_max32((uint32_t)(b >> 32));
     const uint32_t mlo = wave_max32((uint32_t)(b >> 32) == mhi ? (uint32_t)b : 0u);
     const uint64_t m = ((uint64_t)mhi << 32) | mlo;
@@ -521,8 +528,12 @@ __global__ __launch_bounds__(256) void k_merge_topk(ScoreParams sp,
       break;
     }
 #pragma unroll
-    for (int r = 0; r < R; ++r)
-      if (h[r] == m) h[r] = 0;
+    for (int j = 0; j < LPL; ++j)
+      if (v[j] == m) {  // keys are unique: one list of one lane
+        const int t = lane + 64 * j;
+        ++h[j];
+        v[j] = h[j] < K ? L[t * K + h[j]] : 0ull;
+      }
     if (lane == 0) {  // canonical position -> node (a position is always < N)
       const int32_t pos = key_node(m, sl, inv);
       out[it] = (uint32_t)pos < (uint32_t)sp.N ? perm[pos] : -1;
@@ -553,16 +564,19 @@ struct TopkL {
     KP_HIP(hipGetLastError());
     const int M = ntiles * sp.n_cand;
     const dim3 mg(blocks(rows, 4));
-#define KP_MG(R)                                                                              \
-  hipLaunchKernelGGL((k_merge_topk<R>), mg, dim3(256), 0, c->stream, sp, c->d.part, ntiles, \
-                     rows_unit, c->d.salt, rows, rows_dev, c->d.perm, cand)
-    if (M <= 128)
+    const size_t lds = (size_t)4 * M * sizeof(uint64_t);  // <= 64 KB (M <= 2,048)
+#define KP_MG(LPL)                                                                       \
+  hipLaunchKernelGGL((k_merge_tour<LPL>), mg, dim3(256), lds, c->stream, sp, c->d.part, \
+                     ntiles, rows_unit, c->d.salt, rows, rows_dev, c->d.perm, cand)
+    if (ntiles <= 64)
+      KP_MG(1);
+    else if (ntiles <= 128)
       KP_MG(2);
-    else if (M <= 256)
+    else if (ntiles <= 256)
       KP_MG(4);
-    else if (M <= 512)
+    else if (ntiles <= 512)
       KP_MG(8);
-    else if (M <= 1024)
+    else if (ntiles <= 1024)
       KP_MG(16);
     else
       KP_MG(32);

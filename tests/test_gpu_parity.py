@@ -303,6 +303,18 @@ def test_fused_wide_scores(oracle, w, mode):
     _assert_same(g, o, f"wide scores w={w}")
 
 
+def test_fused_many_tiles_parity(oracle):
+    """More than 64 tiles per row (70k nodes): the merge holds two lists per
+    lane."""
+    w = few_class_workload(77, J=1200, N=70_000, D=4, classes=3, affinity=False)
+    p = _abi.default_params(n_cand=8)
+    with Placer(device=0) as pl:
+        g = pl.place(w, p)
+        assert pl.timing()["fused"] == 1
+    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
+    _assert_same(g, o, "many tiles")
+
+
 @pytest.mark.parametrize("mpm", [512 * 900, 640 * 3000])
 def test_materialised_chunked_parity(oracle, monkeypatch, mpm):
     """The materialised candidate phase with a score matrix chunked into
