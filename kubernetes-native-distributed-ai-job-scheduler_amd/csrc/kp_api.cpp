@@ -331,6 +331,7 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = std::getenv("KP_FZ_WG_TARGET")) c->fz_wg_target = std::max(64, std::atoi(e));
   if (const char *e = std::getenv("KP_COUNT_DIRECT")) c->count_direct = std::atoi(e) != 0;
   if (const char *e = std::getenv("KP_FZ_H16")) c->fz_h16 = std::atoi(e) != 0;
+  if (const char *e = std::getenv("KP_FZ_TIE_BITS")) c->fz_tie_bits = std::max(0, std::min(31, std::atoi(e)));
   if (const char *e = std::getenv("KP_FZ_PROF"))  // phase clocks (KP_FZ_PROFILE builds only)
     if (std::atoi(e) != 0 && hipMalloc(reinterpret_cast<void **>(&c->d.fz_prof), 16 * 8) == hipSuccess)
       (void)hipMemset(c->d.fz_prof, 0, 16 * 8);
@@ -871,7 +872,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
       const int64_t lists = (int64_t)(c->fz_P / 1024) * K * 8;
       tm.score_bytes += rows * ((int64_t)8 * c->D + 12 + lists) +
                         (int64_t)(2 * c->D + 3) * 4 * c->fz_P;
-      tm.select_bytes += rows * (lists + K * 4);  // k_merge_topk
+      tm.select_bytes += rows * (lists + K * 4);  // k_merge_tour
     } else {
       tm.score_bytes += rows * Ns * 4 + (int64_t)8 * c->D * rows + (int64_t)3 * 8 * c->D * N +
                         8 * (int64_t)N;

@@ -156,6 +156,7 @@ struct kp_ctx {
   int32_t score_wg_target = 4096, score_min_rpb = 4, score_npl = 2;
   int32_t fz_wg_target = 2048;  // KP_FZ_WG_TARGET: target workgroups of k_score_topk
   bool fz_h16 = true;     // KP_FZ_H16=0: 32-bit LDS scores in k_score_topk
+  int32_t fz_tie_bits = 0;  // KP_FZ_TIE_BITS=b (tests): b select-phase tie bits, forces collisions
   int32_t acc_list = 1;  // KP_ACC_LIST=0: k_accept walks every node while entries >= nodes
   // KP_COMPACT_MAX: largest unit range compacted by the one-workgroup kernel
   int32_t compact_max = 262144;

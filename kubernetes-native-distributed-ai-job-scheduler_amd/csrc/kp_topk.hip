@@ -70,7 +70,7 @@ constexpr int kFzBS = 64 * kFzWaves;
 constexpr int kFzTile = 128 * kFzWaves;  // columns per workgroup (2 per lane)
 constexpr int kFzRC = 8;                 // rows per LDS chunk: one per wave in the select
 constexpr int kFzMaxRows = 128;          // rows per workgroup (request stage)
-constexpr int kFzSurv = 64;              // survivor slots per wave
+constexpr int kFzSurv = 128;             // survivor slots per wave (2 per lane)
 
 template <int D>
 constexpr int fz_dp() {
@@ -157,7 +157,7 @@ void k_score_topk(
     ScoreParams sp, const uint32_t *__restrict__ np, int32_t P, const int64_t *__restrict__ q,
     int32_t qstride, const int32_t *__restrict__ uaff, const uint32_t *__restrict__ salt,
     const int32_t *__restrict__ rows_unit, int32_t rows, int32_t rows_per_block, int32_t min_rpb,
-    const int32_t *__restrict__ rows_dev, const int32_t *__restrict__ wshift, int32_t ksh,
+    const int32_t *__restrict__ rows_dev, const int32_t *__restrict__ wshift, int32_t ksh, int32_t tbits,
     uint64_t *__restrict__ part, uint64_t *__restrict__ prof) {
   constexpr int DP = fz_dp<D>();  // lanes per row in the threshold stage
   constexpr int SQW = D + 3;      // per row: requests, GPU request, affinity domain, tie salt
@@ -170,6 +170,7 @@ void k_score_topk(
   __shared__ uint32_t sq[kFzMaxRows][SQW];
   __shared__ uint64_t sbuf[kFzWaves][kFzSurv];
   __shared__ uint32_t spos[kFzTile / 4];
+  __shared__ uint32_t spos0[kFzTile / 4];  // tie mode 0: the select-phase tie bits
   __shared__ uint8_t scand[kFzWaves][64];  // per wave: lanes whose best reached T
   constexpr int RW = (2 * D + 4 + 3) & ~3;  // row record words, whole 16-B reads
   __shared__ __attribute__((aligned(16))) uint32_t srec[kFzWaves][kFzRC][RW];
@@ -240,9 +241,18 @@ void k_score_topk(
   // tile): their canonical positions times the tie multiplier (padding
   // columns get garbage, they are never feasible)
   const uint32_t mul = sp.tie_rotated ? kTieMul : 1u;
+  // Tie mode 0 (tie = position): the tile's real columns hold positions
+  // p0 .. p0 + 1023 (p0 = its first column's), so the select phase ranks
+  // ties by p0 + 1023 - pos in the top 10 bits, not by the top bits of
+  // ~pos (which are equal across the tile and send ties to the bisection).
+  // Monotone in the exact key, so the survivor bound stays exact; padding
+  // columns wrap mod 1024 and stay below 1 << ksh.
+  const bool tie0 = !sp.tie_rotated;
   if (tid < kFzTile / 4) {
     const int c = tile0 + 4 * tid;
-    spos[tid] = (uint32_t)(c - wshift[c >> 7]) * mul;
+    const uint32_t pos = (uint32_t)(c - wshift[c >> 7]);
+    spos[tid] = pos * mul;
+    spos0[tid] = pos << 22;
   }
   KP_FZ_PROF_MARK(0);
   __syncthreads();  // requests and positions staged
@@ -252,7 +262,7 @@ void k_score_topk(
 #pragma unroll
   for (int d = 0; d < D; ++d) wv[d] = in_vgpr(sp.w[d]);
   const int32_t waffv = in_vgpr(sp.w_affinity);
-  const int rsh = 32 - ksh;
+  const int rsh = 32 - tbits;  // select-phase tie bits: tbits <= ksh (= ksh but in tests)
   for (int c0 = 0; c0 < nr; c0 += kFzRC) {
     const int cr = min(kFzRC, nr - c0);
     const int buf = H16 ? (c0 / kFzRC) & 1 : 0;
@@ -370,16 +380,19 @@ void k_score_topk(
       const int i = wave;
       const int64_t row = r0 + c0 + i;
       const uint32_t nsl = ~sq[c0 + i][D + 2];
+      // select-phase tie bits: (nst - tsp[g] - j * mt) >> rsh
+      const uint32_t *tsp = tie0 ? spos0 : spos;
+      const uint32_t nst = tie0 ? (spos[0] + 1023u) << 22 : nsl, mt = tie0 ? 1u << 22 : mul;
       uint32_t best = 0;
 #pragma unroll 1
       for (int k = 0; k < 4; ++k) {
         uint32_t v4[4];
         load_group<H16>(ssc[buf][i], lane + 64 * k, v4);
-        const uint32_t npk = nsl - spos[lane + 64 * k];
+        const uint32_t npk = nst - tsp[lane + 64 * k];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const uint32_t s1 = v4[j];
-          best = max(best, (s1 << ksh) | ((npk - (uint32_t)j * mul) >> rsh));
+          best = max(best, (s1 << ksh) | ((npk - (uint32_t)j * mt) >> rsh));
         }
       }
       // T = the K-th largest lane best (radix select over ballots; lower
@@ -417,7 +430,7 @@ void k_score_topk(
           const int g = L + 64 * ((e >> 2) & 3), jj = e & 3;  // its column group, column
           s1 = load_one<H16>(srow, 4 * g + jj);
           ntk = nsl - spos[g] - (uint32_t)jj * mul;
-          hit = ((s1 << ksh) | (ntk >> rsh)) >= T;
+          hit = ((s1 << ksh) | ((nst - tsp[g] - (uint32_t)jj * mt) >> rsh)) >= T;
         }
         const uint64_t mm = __ballot(hit);
         const int p = C + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32),
@@ -426,7 +439,7 @@ void k_score_topk(
         C += __popcll(mm);
       }
       if (C > kFzSurv) {
-        // exact K-th largest 64-bit key by bisection (> 64 keys reached T:
+        // exact K-th largest 64-bit key by bisection (> 128 keys reached T:
         // adversarial ties; the columns are re-read from LDS)
         uint64_t pre = 0;
 #pragma unroll 1
@@ -462,18 +475,39 @@ void k_score_topk(
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       KP_FZ_PROF_MARK(7);
-      // exact rank of each survivor (one per lane; keys broadcast with
-      // v_readlane, no LDS round trip per step); ranks < K are the list
-      const uint64_t my = lane < C ? sbuf[wave][lane] : 0ull;
-      const uint32_t mlo = (uint32_t)my, mhi = (uint32_t)(my >> 32);
-      int r = 0;
-      for (int j = 0; j < C; ++j) {
-        const uint64_t o = ((uint64_t)rl(mhi, j) << 32) | rl(mlo, j);
-        r += o > my ? 1 : 0;
-      }
+      // exact rank of each survivor (one per lane, two past 64; keys
+      // broadcast with v_readlane, no LDS round trip per step); ranks < K
+      // are the list
       uint64_t *dst = part + (row * ntiles + tile) * K;
-      if (lane < C && r < K) dst[r] = my;
-      if (lane >= C && lane < K) dst[lane] = 0ull;
+      if (C <= 64) {
+        const uint64_t my = lane < C ? sbuf[wave][lane] : 0ull;
+        const uint32_t mlo = (uint32_t)my, mhi = (uint32_t)(my >> 32);
+        int r = 0;
+        for (int j = 0; j < C; ++j) {
+          const uint64_t o = ((uint64_t)rl(mhi, j) << 32) | rl(mlo, j);
+          r += o > my ? 1 : 0;
+        }
+        if (lane < C && r < K) dst[r] = my;
+        if (lane >= C && lane < K) dst[lane] = 0ull;
+      } else {  // 64 < C <= 128 (K <= 64 < C: every slot is filled)
+        const uint64_t my0 = sbuf[wave][lane];
+        const uint64_t my1 = lane + 64 < C ? sbuf[wave][lane + 64] : 0ull;
+        const uint32_t alo = (uint32_t)my0, ahi = (uint32_t)(my0 >> 32);
+        const uint32_t blo = (uint32_t)my1, bhi = (uint32_t)(my1 >> 32);
+        int r0 = 0, r1 = 0;
+        for (int j = 0; j < 64; ++j) {
+          const uint64_t o = ((uint64_t)rl(ahi, j) << 32) | rl(alo, j);
+          r0 += o > my0 ? 1 : 0;
+          r1 += o > my1 ? 1 : 0;
+        }
+        for (int j = 64; j < C; ++j) {
+          const uint64_t o = ((uint64_t)rl(bhi, j - 64) << 32) | rl(blo, j - 64);
+          r0 += o > my0 ? 1 : 0;
+          r1 += o > my1 ? 1 : 0;
+        }
+        if (r0 < K) dst[r0] = my0;
+        if (lane + 64 < C && r1 < K) dst[r1] = my1;
+      }
     }
     KP_FZ_PROF_MARK(8);
     if constexpr (!H16) __syncthreads();  // the single LDS tile is rewritten next
@@ -549,10 +583,11 @@ struct TopkL {
     const int64_t want = ((int64_t)rows * ntiles + c->fz_wg_target - 1) / c->fz_wg_target;
     const int rpb = (int)std::min<int64_t>(kFzMaxRows, std::max<int64_t>(kFzRC, want));
     const dim3 grid(ntiles, blocks(rows, rpb));
+    const int32_t tb = c->fz_tie_bits > 0 ? std::min(ksh, c->fz_tie_bits) : ksh;
 #define KP_FZ(M, H)                                                                              \
   hipLaunchKernelGGL((k_score_topk<D, M, H>), grid, dim3(kFzBS), 0, c->stream, sp, c->d.np32, P, \
                      c->d.q, c->U, c->d.aff, c->d.salt, rows_unit, rows, rpb, kFzRC, rows_dev,    \
-                     c->d.wshift, ksh, c->d.part, c->d.fz_prof)
+                     c->d.wshift, ksh, tb, c->d.part, c->d.fz_prof)
     // 16-bit LDS scores when every score + 1 < 2^16 (ksh >= 16)
     const bool h16 = ksh >= 16 && c->fz_h16;
     if (sp.most_allocated) {

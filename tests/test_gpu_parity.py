@@ -331,9 +331,9 @@ def test_materialised_chunked_parity(oracle, monkeypatch, mpm):
 
 @pytest.mark.parametrize("tie", [0, 1])
 def test_fused_all_equal_nodes(oracle, tie):
-    """Identical empty nodes: every column of a tile ties on score, so the
-    32-bit keys cannot separate the survivors (tie_mode 0) and the exact
-    bisection path selects the tile's top-K."""
+    """Identical empty nodes: every column of a tile ties on score and only
+    the tie keys separate them (tie_mode 0: the tile-relative position bits
+    of the select phase; tie_mode 1: the top bits of the rotated key)."""
     N, J = 3000, 400
     cap = np.tile(np.array([[64000], [262144], [8], [1 << 20]], np.int64), (1, N))
     w = synth.Workload(J, N, 4, np.tile(np.array([[1000], [4096], [1], [1 << 16]], np.int64), (1, J)),
@@ -803,3 +803,20 @@ def test_create_multi_streaming(oracle):
             done = np.nonzero(g["node"] >= 0)[0][::3]
             pl.apply_delta(g["node"][done], -rq[:, done])
             np.subtract.at(used_o.T, g["node"][done], rq[:, done].T)
+
+
+@pytest.mark.parametrize("tie", [0, 1])
+@pytest.mark.parametrize("bits,K", [(1, 16), (1, 32), (3, 32), (5, 32), (8, 8)])
+def test_fused_key_collisions(oracle, monkeypatch, tie, bits, K):
+    """Fewer tie bits in the select phase's 32-bit keys (KP_FZ_TIE_BITS, a
+    test knob) make keys collide: more survivors than one per lane (two-per-
+    lane rank, up to 128) and more than 128 (exact 64-bit bisection). The
+    lists stay exact."""
+    monkeypatch.setenv("KP_FZ_TIE_BITS", str(bits))
+    w = few_class_workload(1300 + 7 * bits + K + tie, J=1500, N=2600, D=3, classes=2)
+    p = _abi.default_params(tie_mode=tie, n_cand=K)
+    with Placer(device=0) as pl:
+        g = pl.place(w, p)
+        assert pl.timing()["fused"] == 1
+    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
+    _assert_same(g, o, f"collisions tie={tie} bits={bits} K={K}")
