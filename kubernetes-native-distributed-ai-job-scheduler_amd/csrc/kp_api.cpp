@@ -43,6 +43,7 @@ void kp_set_error_msg(const std::string &msg) {
 }
 
 namespace kp {
+constexpr int kProfWords = 16 + 64 + 4 * 1024;  // fz_prof: fused phases + pass profile
 
 // Entry guard of every public call: the context lock for the whole call, the
 // per-context error slot, and the context's device on this thread.
@@ -333,8 +334,12 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = std::getenv("KP_FZ_H16")) c->fz_h16 = std::atoi(e) != 0;
   if (const char *e = std::getenv("KP_FZ_TIE_BITS")) c->fz_tie_bits = std::max(0, std::min(31, std::atoi(e)));
   if (const char *e = std::getenv("KP_FZ_PROF"))  // phase clocks (KP_FZ_PROFILE builds only)
-    if (std::atoi(e) != 0 && hipMalloc(reinterpret_cast<void **>(&c->d.fz_prof), 16 * 8) == hipSuccess)
-      (void)hipMemset(c->d.fz_prof, 0, 16 * 8);
+    if (std::atoi(e) != 0 && hipMalloc(reinterpret_cast<void **>(&c->d.fz_prof), kProfWords * 8) == hipSuccess) {
+      // [16 + 64 + 4 L + {0, 2}]: minima of the pass-profile launch stamps
+      std::vector<uint64_t> h(kProfWords, 0);
+      for (int L = 0; L < 1024; ++L) h[16 + 64 + 4 * L] = h[16 + 64 + 4 * L + 2] = ~0ull;
+      (void)hipMemcpy(c->d.fz_prof, h.data(), kProfWords * 8, hipMemcpyHostToDevice);
+    }
   if (hipSetDevice(dev) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void **>(&c->pinned), 4096, hipHostMallocDefault) !=
@@ -1015,11 +1020,26 @@ void kp_destroy(kp_ctx *c) {
   if (c->nccl_comm) ncclCommDestroy(static_cast<ncclComm_t>(c->nccl_comm));
   DevState &d = c->d;
   if (d.fz_prof) {  // KP_FZ_PROF: the accumulated phase clocks
-    uint64_t h[16] = {0};
-    if (hipMemcpy(h, d.fz_prof, sizeof h, hipMemcpyDeviceToHost) == hipSuccess) {
+    std::vector<uint64_t> h(kProfWords, 0);
+    if (hipMemcpy(h.data(), d.fz_prof, kProfWords * 8, hipMemcpyDeviceToHost) == hipSuccess) {
       std::fprintf(stderr, "kp_fz_prof");
       for (int i = 0; i < 9; ++i) std::fprintf(stderr, " %llu", (unsigned long long)h[i]);
       std::fprintf(stderr, "\n");
+      const uint64_t *pp = h.data() + 16;  // KP_PASS_PROFILE (kp_pass.hip)
+      for (int k = 0; k < 2; ++k) {
+        const uint64_t *b = pp + 16 * k;
+        std::fprintf(stderr, "kp_pass_prof %s waves %llu working %llu phase_clk", k ? "accept" : "plan",
+                     (unsigned long long)b[8], (unsigned long long)b[9]);
+        for (int i = 0; i < 8; ++i) std::fprintf(stderr, " %llu", (unsigned long long)b[i]);
+        double span = 0;
+        int n = 0;
+        for (int L = 0; L < 1024; ++L) {
+          const uint64_t lo = pp[64 + 4 * L + 2 * k], hi = pp[64 + 4 * L + 2 * k + 1];
+          if (lo != ~0ull && hi >= lo) { span += (double)(hi - lo) * 0.01; ++n; }
+        }
+        std::fprintf(stderr, " launches %d span_us %.1f wave_clk %llu wave_rt %llu\n", n, span,
+                     (unsigned long long)b[10], (unsigned long long)b[11]);
+      }
     }
   }
   void *ptrs[] = {d.cap, d.used, d.used0, d.R32, d.K32, d.base, d.topo, d.q, d.leader, d.size,

@@ -37,6 +37,65 @@ namespace kp {
 namespace {
 using namespace dev;
 
+// KP_PASS_PROFILE (a timing build, with KP_FZ_PROF=1): per-phase shader
+// clocks of every plan / accept wave (each mark waits for the wave's
+// outstanding memory operations, so a phase owns its load latency), and the
+// first-wave-start / last-wave-end real-time stamps of every launch.
+// Layout of pp = fz_prof + 16: [0..7] plan phase sums, [8] plan waves, [9]
+// plan waves with open slots; [16..23], [24], [25] the same for accept;
+// [64 + 4 L + {0,1,2,3}] plan min start, plan max end, accept min start,
+// accept max end of launch L = round * 16 + pass (L < 1024).
+#ifdef KP_PASS_PROFILE
+struct PassProf {
+  uint64_t *pp;
+  int base, slot, lane;
+  uint64_t t_prev, t_first, r_first, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  bool work = false;
+  // one wave in 8 workgroups records (contended atomics would serialise)
+  __device__ PassProf(uint64_t *p, int b, int L)
+      : pp((blockIdx.x & 7) == 0 && threadIdx.x < 64 ? p : nullptr), base(b), slot(L),
+        lane(threadIdx.x & 63) {
+    t_prev = t_first = __builtin_amdgcn_s_memtime();
+    r_first = __builtin_amdgcn_s_memrealtime();
+    if (pp && lane == 0 && slot < 1024)
+      atomicMin((unsigned long long *)&pp[64 + 4 * slot + (base ? 2 : 0)],
+                (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
+  __device__ void mark(int ph) {
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    acc[ph] += now - t_prev;
+    t_prev = now;
+  }
+  __device__ ~PassProf() {
+    mark(7);
+    if (!pp || lane != 0) return;
+    for (int i = 0; i < 8; ++i) atomicAdd((unsigned long long *)&pp[base + i], (unsigned long long)acc[i]);
+    atomicAdd((unsigned long long *)&pp[base + 8], 1ull);
+    if (work) atomicAdd((unsigned long long *)&pp[base + 9], 1ull);
+    atomicAdd((unsigned long long *)&pp[base + 10], (unsigned long long)(t_prev - t_first));
+    atomicAdd((unsigned long long *)&pp[base + 11],
+              (unsigned long long)(__builtin_amdgcn_s_memrealtime() - r_first));
+    if (slot < 1024)
+      atomicMax((unsigned long long *)&pp[64 + 4 * slot + (base ? 3 : 1)],
+                (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
+};
+#define KP_PP_DECL(P, B, L) PassProf pp_(P, B, L)
+#define KP_PP_MARK(ph) pp_.mark(ph)
+#define KP_PP_WORK() (pp_.work = true)
+#else
+#define KP_PP_DECL(P, B, L) \
+  do {                      \
+  } while (0)
+#define KP_PP_MARK(ph) \
+  do {                 \
+  } while (0)
+#define KP_PP_WORK() \
+  do {               \
+  } while (0)
+#endif
+
 constexpr uint32_t kNoBid = 0xFFFFFFFFu;  // tag that matches no pass
 
 // ---- inverse index (once per round) --------------------------------------------
@@ -153,6 +212,8 @@ struct PlanArgs {
   int32_t *win, *s0_out, *pass_flag;
   int4 *gpart;
   int32_t *nparts, *arrive, *node_flag;
+  uint64_t *pp;            // KP_PASS_PROFILE only
+  const SolveStats *st;    // KP_PASS_PROFILE only (round index)
 };
 
 // the slots of wave `wave_global` (whole wave). The slot loads do not wait
@@ -163,6 +224,9 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
   constexpr int SPW = 64 / G;  // slots per wave
   constexpr uint64_t GMASK = G == 64 ? ~0ull : ((1ull << G) - 1);
   const ScoreParams &sp = pa.sp;
+#ifdef KP_PASS_PROFILE
+  KP_PP_DECL(pa.pp, 0, pa.pp ? (int)(pa.st->rounds - 1) * 16 + pass : 1024);
+#endif
   const int lane = threadIdx.x & 63;
   const int gl = lane & (G - 1);      // lane within the group = candidate index
   const int gbase = lane & ~(G - 1);  // first lane of the group
@@ -180,7 +244,9 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
   if (!prev) return;
   const bool in = a < A;
   const bool slot_ok = in && op;
+  KP_PP_MARK(0);
   if (__ballot(slot_ok) == 0) return;
+  KP_PP_WORK();
   const int32_t u = slot_ok ? u0 : 0;
   const int32_t sz = slot_ok ? pa.size[u] : 0;
   const int32_t af = slot_ok ? pa.aff[u] : -1;
@@ -213,6 +279,7 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
     const int32_t b = (int32_t)pa.base[nn];
     const int g = sp.gpu_dim;
     const int32_t abonus = (af >= 0 && tp == af) ? sp.w_affinity : 0;
+    KP_PP_MARK(1);
     for (int m = 0; m < szmax; ++m) {
       const bool live = !fail && m < sz;  // group-uniform
       bool fits = live && valid;
@@ -275,6 +342,7 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
       }
     }
   }
+  KP_PP_MARK(2);
   // group-uniform from here on (slot_ok and fail are per group)
   const bool prop = slot_ok && !fail && gl < K && planned > 0;
   const uint64_t pm = (__ballot(prop) >> gbase) & GMASK;
@@ -459,6 +527,8 @@ struct AccArgs {
   const int64_t *winmin;
   int64_t nwin;
   AcceptOut o;
+  uint64_t *pp;            // KP_PASS_PROFILE only
+  const SolveStats *st;    // KP_PASS_PROFILE only (round index)
 };
 
 // the bidders of `node` in pass `pass` (whole wave). Flagged windows whose
@@ -470,6 +540,9 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
   const int lane = threadIdx.x & 63;
   const int N = ac.sp.N;
   const AcceptOut &o = ac.o;
+#ifdef KP_PASS_PROFILE
+  KP_PP_DECL(ac.pp, 16, ac.pp ? (int)(ac.st->rounds - 1) * 16 + pass : 1024);
+#endif
   const int32_t nf = ac.node_flag[node];
 #if KP_ACC_FLAG_FIRST  // A/B: test the node flag before loading the node's operands
   if (nf != pass) return;
@@ -482,7 +555,9 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
     rem[d] = ac.cap[(int64_t)d * N + node] - o.used[(int64_t)d * N + node];
     add[d] = 0;
   }
+  KP_PP_MARK(0);
   if (nf != pass || e0 < 0) return;  // nobody bid on this node in this pass
+  KP_PP_WORK();
   const int32_t w0 = e0 >> 6, w1 = (e1 - 1) >> 6;
   constexpr int BATCH = 4;  // flagged windows whose operands are loaded together
   for (int wb = w0; wb <= w1; wb += 64) {
@@ -493,6 +568,7 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
 #pragma unroll
     for (int d = 0; d < D; ++d) wmin[d] = mine ? ac.winmin[(int64_t)d * ac.nwin + wi] : 0;
     uint64_t flagged = w0 == w1 ? 1ull : __ballot(mine && ac.win[wi] == pass);
+    KP_PP_MARK(1);
     while (true) {
       bool can = true;
 #pragma unroll
@@ -510,11 +586,13 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
       for (int t = 0; t < BATCH; ++t)
         load_win<D>(wv[t], wl[t], lane, e0, e1, pass, ac.P, ac.bid, ac.ent_q, ac.ent_unit,
                     ac.ent_size, ac.ent_lead, ac.ent_slot, ac.s0);
+      KP_PP_MARK(2);
 #pragma unroll
       for (int t = 0; t < BATCH; ++t) {
         if (wl[t] < 0) break;
         decide_window<D>(wv[t], rem, add, lane, node, o);
       }
+      KP_PP_MARK(3);
     }
   }
   // fold the single-node units committed by this wave into `used`
@@ -574,6 +652,8 @@ static PlanArgs plan_args(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t p
   pa.nparts = c->d.nparts;
   pa.arrive = c->d.arrive;
   pa.node_flag = c->d.node_flag;
+  pa.pp = c->d.fz_prof ? c->d.fz_prof + 16 : nullptr;
+  pa.st = c->d.stats;
   return pa;
 }
 
@@ -611,6 +691,8 @@ static AccArgs acc_args(kp_ctx *c, const ScoreParams &sp, int64_t P) {
   o.status = c->d.status;
   o.job_node = c->d.job_node;
   o.job_score = c->d.job_score;
+  ac.pp = c->d.fz_prof ? c->d.fz_prof + 16 : nullptr;
+  ac.st = c->d.stats;
   return ac;
 }
 

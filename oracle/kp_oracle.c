@@ -11,6 +11,7 @@
  */
 #include "kp_oracle.h"
 
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -394,6 +395,8 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
   }
   st->pairs += (int64_t)active0 * N;
 
+  const int trace = getenv("KPO_TRACE") != NULL; /* per-round counts on stderr (analysis) */
+  int32_t passes0 = st->passes;
   for (int pass = 0; pass < st->p.max_passes; ++pass) {
     /* proposals of every open unit, planned against the current usage */
     int32_t np = 0;
@@ -447,6 +450,8 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
       open[u] = 0;
     }
   }
+  if (trace)
+    fprintf(stderr, "kpo round %d active %d passes %d\n", st->rounds, active0, st->passes - passes0);
   st->rounds++;
   free(open); free(props); free(ok); free(gang_bad);
   return kpo_state_active(st);
