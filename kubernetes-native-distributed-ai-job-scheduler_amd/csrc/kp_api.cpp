@@ -331,6 +331,7 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = std::getenv("KP_ACC_LIST")) c->acc_list = std::atoi(e);
   if (const char *e = std::getenv("KP_FZ_WG_TARGET")) c->fz_wg_target = std::max(64, std::atoi(e));
   if (const char *e = std::getenv("KP_COUNT_DIRECT")) c->count_direct = std::atoi(e) != 0;
+  if (const char *e = std::getenv("KP_HOST_PROF")) c->host_prof = std::atoi(e) != 0;
   if (const char *e = std::getenv("KP_FZ_H16")) c->fz_h16 = std::atoi(e) != 0;
   if (const char *e = std::getenv("KP_FZ_TIE_BITS")) c->fz_tie_bits = std::max(0, std::min(31, std::atoi(e)));
   if (const char *e = std::getenv("KP_FZ_PROF"))  // phase clocks (KP_FZ_PROFILE builds only)
@@ -769,7 +770,17 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     int64_t A_bound = shard;
     // the round's count: stored by the compaction kernel into coherent pinned
     // memory (spin on the -1 sentinel), or copied + event
+    double wait_us = 0;
+    const auto h_start = std::chrono::steady_clock::now();
     auto round_count = [&](bool direct) -> int {
+      const auto w0 = std::chrono::steady_clock::now();
+      struct WaitAcc {
+        double &acc;
+        std::chrono::steady_clock::time_point t;
+        ~WaitAcc() {
+          acc += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t).count();
+        }
+      } wacc{wait_us, w0};
       if (!direct) {
         KP_HIP(hipEventSynchronize(evA));
         return KP_OK;
@@ -811,6 +822,15 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
       KP_TRY(round_count(direct));  // landed long ago on a busy round
       round_active.push_back(*A_h);
       A_bound = *A_h;
+      if (c->host_prof) {
+        const double now = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h_start).count();
+        std::fprintf(stderr, "kp_host_round %d A %d t_us %.1f wait_us %.1f\n", r, *A_h, now, wait_us);
+      }
+    }
+    if (c->host_prof) {
+      const double tot = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h_start).count();
+      std::fprintf(stderr, "kp_host_prof rounds %zu host_loop_us %.1f wait_us %.1f enqueue_us %.1f\n",
+                   round_active.size(), tot, wait_us, tot - wait_us);
     }
   } else {
     // Multi-GPU, device-driven like the single-GPU loop: the local and the
@@ -856,6 +876,10 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   }
   KP_TRY(launch_finalize(c));
   KP_HIP(hipEventRecord(t1, c->stream));
+  if (c->host_prof && c->world == 1) {
+    launch_probe(c, sp, std::min<int32_t>(shard, 26000));
+    launch_probe(c, sp, std::min<int32_t>(shard, 1000));
+  }
   // per-unit status and the device-side statistics
   std::vector<int32_t> status(U);
   if (U > 0)
@@ -1022,6 +1046,14 @@ void kp_destroy(kp_ctx *c) {
   if (d.fz_prof) {  // KP_FZ_PROF: the accumulated phase clocks
     std::vector<uint64_t> h(kProfWords, 0);
     if (hipMemcpy(h.data(), d.fz_prof, kProfWords * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+      if (std::getenv("KP_PASS_SPANS"))
+        for (int L = 0; L < 1024; ++L) {
+          const uint64_t *x = h.data() + 16 + 64 + 4 * L;
+          if (x[0] == ~0ull || x[2] == ~0ull) continue;
+          std::fprintf(stderr, "kp_pass_span %d %d plan %.2f acc %.2f gap %.2f\n", L / 16, L % 16,
+                       (double)(x[1] - x[0]) * 0.01, (double)(x[3] - x[2]) * 0.01,
+                       ((double)x[2] - (double)x[1]) * 0.01);
+        }
       std::fprintf(stderr, "kp_fz_prof");
       for (int i = 0; i < 9; ++i) std::fprintf(stderr, " %llu", (unsigned long long)h[i]);
       std::fprintf(stderr, "\n");

@@ -192,6 +192,7 @@ struct kp_ctx {
   // count into (KP_COUNT_DIRECT=0: copy it with hipMemcpyAsync instead)
   int32_t *pinned_coh = nullptr;
   bool count_direct = true;
+  bool host_prof = false;  // KP_HOST_PROF=1: host enqueue / wait split per solve on stderr
   kp::DevState d;
   // what the next node-plane pack builds: the solve's canonical column order
   // (scores by perm[column]) or kp_score's node order, for these params
@@ -234,6 +235,7 @@ int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass,
 int launch_active_async(kp_ctx *c, int32_t lo, int32_t hi, int32_t *count_host,
                         bool *direct = nullptr);
 int launch_accept(kp_ctx *c, const ScoreParams &sp, int32_t pass, int32_t A);
+void launch_probe(kp_ctx *c, const ScoreParams &sp, int32_t A);
 int launch_active(kp_ctx *c, int32_t lo, int32_t hi, int32_t *A_host);
 int launch_reset_units(kp_ctx *c);
 int launch_finalize(kp_ctx *c);

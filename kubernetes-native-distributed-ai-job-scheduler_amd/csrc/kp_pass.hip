@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 
 #include <rocprim/rocprim.hpp>
@@ -794,6 +795,45 @@ int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass, const
 int launch_accept(kp_ctx *c, const ScoreParams &sp, int32_t pass, int32_t A) {
   if (c->N <= 0 || A <= 0) return KP_OK;
   return dispatch_D<AcceptL>(c->D, c, sp, pass, (int64_t)A * sp.n_cand);
+}
+
+// KP_HOST_PROF probe: GPU time per launch of dependent no-op launches on the
+// library's stream (host far ahead): a trivial 1-WG kernel, and pass launches
+// whose pass flag is clear (plan and accept exit after their first loads).
+__global__ void k_probe_noop(int32_t *p) {
+  if (p[threadIdx.x & 15] == 12345) p[threadIdx.x & 15] = 0;  // counters[40..55]
+}
+
+__global__ void k_probe_spin(uint64_t ticks) {  // s_memrealtime: 100 MHz
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(10);
+}
+
+void launch_probe(kp_ctx *c, const ScoreParams &sp, int32_t A) {
+  if (A <= 0 || c->N <= 0) return;
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return;
+  const int L = 400;
+  for (int kind = 0; kind < 4; ++kind) {
+    (void)hipStreamSynchronize(c->stream);
+    // queue a backlog first so that the host is ahead of the timed launches
+    hipLaunchKernelGGL(k_probe_spin, dim3(1), dim3(64), 0, c->stream, (uint64_t)1000000);  // 10 ms
+    (void)hipEventRecord(e0, c->stream);
+    for (int i = 0; i < L; ++i) {
+      if (kind == 0) hipLaunchKernelGGL(k_probe_noop, dim3(1), dim3(64), 0, c->stream, c->d.counters + 40);
+      if (kind == 1) (void)launch_plan(c, sp, A, 63, c->d.counters);
+      if (kind == 2) (void)launch_accept(c, sp, 63, A);
+      if (kind == 3) (void)launch_plan(c, sp, 1, 63, c->d.counters);
+    }
+    (void)hipEventRecord(e1, c->stream);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    static const char *nm[] = {"noop-1wg", "dead-plan", "dead-accept", "dead-plan-1wg"};
+    std::fprintf(stderr, "kp_probe %s A %d: %.2f us/launch\n", nm[kind], A, ms * 1e3 / L);
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
 }
 
 }  // namespace kp
