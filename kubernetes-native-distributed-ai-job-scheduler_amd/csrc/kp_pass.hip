@@ -47,6 +47,9 @@ using namespace dev;
 // [64 + 4 L + {0,1,2,3}] plan min start, plan max end, accept min start,
 // accept max end of launch L = round * 16 + pass (L < 1024).
 #ifdef KP_PASS_PROFILE
+#ifndef KP_PASS_PROFILE_MINROUND
+#define KP_PASS_PROFILE_MINROUND 0  // rounds below are not sampled
+#endif
 struct PassProf {
   uint64_t *pp;
   int base, slot, lane;
@@ -54,7 +57,8 @@ struct PassProf {
   bool work = false;
   // one wave in 8 workgroups records (contended atomics would serialise)
   __device__ PassProf(uint64_t *p, int b, int L)
-      : pp((blockIdx.x & 7) == 0 && threadIdx.x < 64 ? p : nullptr), base(b), slot(L),
+      : pp((blockIdx.x & 7) == 0 && threadIdx.x < 64 && L / 16 >= KP_PASS_PROFILE_MINROUND ? p : nullptr),
+        base(b), slot(L),
         lane(threadIdx.x & 63) {
     t_prev = t_first = __builtin_amdgcn_s_memtime();
     r_first = __builtin_amdgcn_s_memrealtime();
