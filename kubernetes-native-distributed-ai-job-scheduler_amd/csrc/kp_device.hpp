@@ -270,6 +270,20 @@ __device__ __forceinline__ uint32_t div_floor32(uint32_t x, uint32_t c, uint32_t
   return t;
 }
 
+// the same exact division with its remainder: x·S = t·c + r, 0 <= r < c
+// (x <= c < 2^32; c = 0 with x = 0 gives t = r = 0)
+__device__ __forceinline__ void divmod32(uint32_t x, uint32_t c, uint32_t R, uint32_t K, uint32_t S,
+                                         uint32_t &t, uint32_t &r) {
+  t = (uint32_t)(((uint64_t)x * R) >> (K & 63u));
+  uint64_t rr = (uint64_t)x * S - (uint64_t)t * c;
+  const uint64_t cc = c ? c : 1;
+  if (rr >= cc) {
+    ++t;
+    rr -= cc;
+  }
+  r = (uint32_t)rr;
+}
+
 // 64-bit form (some cap >= 2^32, caps <= 2^56): x*S needs up to 67 bits. A
 // double estimate (|error| << 1) corrected with 128-bit remainders.
 __device__ __forceinline__ int64_t util64(int64_t x, int64_t c, int32_t S, bool most) {
@@ -347,6 +361,27 @@ __device__ __forceinline__ int32_t group_max_i32(int32_t v) {
     return l < 32 ? m0 : m1;
   }
   return __builtin_amdgcn_readlane(v, 63);
+}
+
+// u32 max over aligned groups of G lanes, returned to every lane of the
+// group: a DPP butterfly inside each 16-lane row (quad xor 1, quad xor 2,
+// half-row mirror, row mirror — each a max with a DPP operand), then the row
+// maxima combined through SGPRs for G = 32 / 64
+template <int G>
+__device__ __forceinline__ uint32_t group_max_u32(uint32_t v) {
+  static_assert(G == 16 || G == 32 || G == 64, "group size");
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false));   // quad [1,0,3,2]
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false));   // quad [2,3,0,1]
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false));  // row_half_mirror
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xf, 0xf, false));  // row_mirror
+  if constexpr (G == 16) {
+    return v;
+  } else {
+    const uint32_t r0 = __builtin_amdgcn_readlane(v, 0), r1 = __builtin_amdgcn_readlane(v, 16);
+    const uint32_t r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
+    if constexpr (G == 32) return lane_id() < 32 ? max(r0, r1) : max(r2, r3);
+    return max(max(r0, r1), max(r2, r3));
+  }
 }
 
 // u32 planes per dim of the packed 32-bit node tile (kp_score.hip pack_node)

@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <type_traits>
 
 #include <rocprim/rocprim.hpp>
 
@@ -217,6 +218,7 @@ struct PlanArgs {
   int32_t *win, *s0_out, *pass_flag;
   int4 *gpart;
   int32_t *nparts, *arrive, *node_flag;
+  uint32_t key_off;        // W32 member loop: 64 * w_spread + 1 (plan_key_ok)
   uint64_t *pp;            // KP_PASS_PROFILE only
   const SolveStats *st;    // KP_PASS_PROFILE only (round index)
 };
@@ -267,56 +269,85 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) szmax = max(szmax, __shfl_xor(szmax, m, kWave));
   if constexpr (W32) {
-    // every cap and request < 2^32 (fits32): the remaining free capacity and
-    // the usage after the planned members are tracked incrementally, so no
-    // product of a member count overflows; the exact division of div_prep
-    // (kp_device.hpp, generic form) and every score fit 32 bits
-    uint32_t q32[D], rem[D], uu[D], cc[D], rr[D], kk[D];
+    // every cap and request < 2^32 (fits32): the remaining free capacity is
+    // tracked incrementally and the utilisation of one more member is
+    // stepped exactly instead of divided again: with (u+q)·S = t·c + r and
+    // q·S = Q·c + ρ (div_prep's exact division, once per lane and dim), one
+    // more planned member gives t += Q + [r ≥ c − ρ], r = (r + ρ) mod c — four
+    // 32-bit operations per dim and member, no 64-bit product in the loop
+    uint32_t q32[D], rem[D], t_[D], r_[D], Q_[D], thr[D], rho[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       q32[d] = (uint32_t)qq[d];
-      uu[d] = (uint32_t)pa.used[(int64_t)d * N + nn];
-      cc[d] = (uint32_t)pa.cap[(int64_t)d * N + nn];
-      rem[d] = cc[d] - uu[d];
-      rr[d] = pa.R32[(int64_t)d * N + nn];
-      kk[d] = pa.K32[(int64_t)d * N + nn];
+      const uint32_t uu = (uint32_t)pa.used[(int64_t)d * N + nn];
+      const uint32_t cc = (uint32_t)pa.cap[(int64_t)d * N + nn];
+      const uint32_t rr = pa.R32[(int64_t)d * N + nn], kk = pa.K32[(int64_t)d * N + nn];
+      rem[d] = cc - uu;
+      // garbage (never used) on a lane where q does not fit: x = u + q may wrap
+      divmod32(uu + q32[d], cc, rr, kk, (uint32_t)sp.S, t_[d], r_[d]);
+      divmod32(q32[d], cc, rr, kk, (uint32_t)sp.S, Q_[d], rho[d]);
+      // c = 0 (then q = 0 on a feasible lane): the dim stays 0, never wraps
+      thr[d] = cc ? cc - rho[d] : 0xFFFFFFFFu;
     }
     const int32_t b = (int32_t)pa.base[nn];
     const int g = sp.gpu_dim;
     const int32_t abonus = (af >= 0 && tp == af) ? sp.w_affinity : 0;
-    KP_PP_MARK(1);
-    for (int m = 0; m < szmax; ++m) {
-      const bool live = !fail && m < sz;  // group-uniform
-      bool fits = live && valid;
-      int32_t acc = 0, bonus = abonus;
+    // Σ_d w_d·t_d, stepped with the utilisations (w_d·Q_d precomputed)
+    int32_t acc_t = 0, wq[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      acc_t += sp.w[d] * (int32_t)t_[d];
+      wq[d] = sp.w[d] * (int32_t)Q_[d];
+    }
+    // score of one more member on this lane's candidate (-1: it does not fit);
+    // changes only when this lane wins a member
+    auto cur_score = [&]() -> int32_t {
+      bool fits = valid;
+      int32_t acc = acc_t, bonus = abonus;
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         fits &= q32[d] <= rem[d];
-        bool nz;
-        const uint32_t t = div_floor32(uu[d] + q32[d], cc[d], rr[d], kk[d], (uint32_t)sp.S, nz);
-        acc += sp.w[d] * (int32_t)(sp.most_allocated ? t : t + (nz ? 1u : 0u));
+        if (!sp.most_allocated && r_[d] != 0) acc += sp.w[d];  // LeastAllocated: ceiling
         if (d == g && q32[d] > 0 && rem[d] == q32[d]) bonus += sp.w_gpu_fit;
       }
-      const int32_t s = fits ? (sp.most_allocated ? acc : b - acc) + bonus : -1;
-      if (m == 0) s0 = s;
-      const bool feas = s >= 0;
-      const int32_t val = feas ? s - sp.w_spread * dom : INT32_MIN;
-      const uint64_t gm = (__ballot(feas) >> gbase) & GMASK;
-      if (live && gm == 0) fail = true;
-      const int32_t best = group_max_i32<G>(val);
-      const uint64_t wm = (__ballot(feas && val == best) >> gbase) & GMASK;
-      const int w = wm ? (__ffsll((unsigned long long)wm) - 1) : 0;
-      const int32_t wtp = __shfl(tp, gbase + w, kWave);
+      return fits ? (sp.most_allocated ? acc : b - acc) + bonus : -1;
+    };
+    int32_t sc = cur_score();
+    s0 = slot_ok ? sc : -1;  // the first member's score at pass-start usage
+    // the group's lanes in this lane's topo domain (the spread penalty counts
+    // members planned into the domain of the winning candidate)
+    uint32_t smask = 0;
+#pragma unroll
+    for (int j = 0; j < G; ++j) smask |= (__shfl(tp, gbase + j, kWave) == tp ? 1u : 0u) << j;
+    KP_PP_MARK(1);
+    // One 32-bit key per lane, (value + off) << log2 G | (G-1-lane): one group
+    // max gives the best value and, among equal values, the lowest lane; key
+    // 0 = infeasible. The host keeps value + off < 2^(32 - log2 G) and off =
+    // 64·w_spread + 1 > any penalty (PlanArgs::key_off).
+    constexpr int LB = G == 16 ? 4 : G == 32 ? 5 : 6;
+    int32_t pen = 0;  // w_spread x members planned into this lane's domain
+    for (int m = 0; m < szmax; ++m) {
+      const bool live = !fail && m < sz;  // group-uniform
+      const uint32_t key = (live && sc >= 0)
+                               ? ((uint32_t)(sc - pen + pa.key_off) << LB) | (uint32_t)(G - 1 - gl)
+                               : 0u;
+      const uint32_t best = group_max_u32<G>(key);
+      if (live && best == 0) fail = true;
       if (live && !fail) {
+        const int w = G - 1 - (int)(best & (G - 1));
         if (gl == w) {
           ++planned;
 #pragma unroll
           for (int d = 0; d < D; ++d) {
             rem[d] -= q32[d];
-            uu[d] += q32[d];
+            const bool wrap = r_[d] >= thr[d];
+            t_[d] += Q_[d] + (wrap ? 1u : 0u);
+            r_[d] = wrap ? r_[d] - thr[d] : r_[d] + rho[d];
+            acc_t += wq[d] + (wrap ? sp.w[d] : 0);
           }
+          sc = cur_score();
         }
-        dom += (valid && tp == wtp) ? 1 : 0;
+        pen += (valid && ((smask >> w) & 1u)) ? sp.w_spread : 0;
       }
     }
   } else {
@@ -398,14 +429,18 @@ __global__ __launch_bounds__(256) void k_plan(PlanArgs pa) {
 // and the first lane that breaks it is rejected (it cannot fit the reduced
 // remainder); repeat on what is left. The operands of the next flagged windows
 // are loaded before the current one is decided (one HBM latency per batch).
-template <int D>
+// N32 (every cap < 2^26, KP_N32_CAP): bid sizes and remaining capacities in
+// 32 bits, so the first-fit prefix sums of a window (at most 64 terms each
+// <= the remaining capacity) are exact 32-bit DPP scans
+template <int D, bool N32>
 struct Win {
+  using NT = typename std::conditional<N32, uint32_t, int64_t>::type;
   int32_t e, m, unit, size, lead, slot, s0;
-  int64_t need[D];
+  NT need[D];
 };
 
-template <int D>
-__device__ __forceinline__ void load_win(Win<D> &w, int wi, int lane, int32_t e0, int32_t e1,
+template <int D, bool N32>
+__device__ __forceinline__ void load_win(Win<D, N32> &w, int wi, int lane, int32_t e0, int32_t e1,
                                          int32_t pass, int64_t P,
                                          const uint32_t *__restrict__ bid,
                                          const int64_t *__restrict__ ent_q,
@@ -424,11 +459,14 @@ __device__ __forceinline__ void load_win(Win<D> &w, int wi, int lane, int32_t e0
   w.lead = ent_lead[ee];
   w.slot = ent_slot[ee];
   w.s0 = s0[ee];
+  int64_t qd[D];
 #pragma unroll
-  for (int d = 0; d < D; ++d) w.need[d] = ent_q[(int64_t)d * P + ee];
+  for (int d = 0; d < D; ++d) qd[d] = ent_q[(int64_t)d * P + ee];
   if (in_row && (t >> 8) == (uint32_t)pass) w.m = (int32_t)(t & 0xFFu);
+  // a bid's members fit the node at plan time: m·q <= cap (< 2^26 with N32)
 #pragma unroll
-  for (int d = 0; d < D; ++d) w.need[d] = w.m > 0 ? (int64_t)w.m * w.need[d] : 0;
+  for (int d = 0; d < D; ++d)
+    w.need[d] = w.m > 0 ? (typename Win<D, N32>::NT)((int64_t)w.m * qd[d]) : 0;
 }
 
 struct AcceptOut {
@@ -467,12 +505,27 @@ __device__ __forceinline__ void commit_gang(const AcceptOut &o, int32_t slot, in
   o.open[slot] = 0;
 }
 
+template <bool N32>
+__device__ __forceinline__ uint32_t scan_excl(uint32_t x) {
+  return (uint32_t)wave_incl_scan_i32((int32_t)x) - x;
+}
+template <bool N32>
+__device__ __forceinline__ int64_t scan_excl(int64_t x) {
+  return wave_incl_scan_i64(x) - x;
+}
+__device__ __forceinline__ uint32_t readlane_nt(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ int64_t readlane_nt(int64_t v, int l) { return readlane_i64(v, l); }
+
 // Exact parallel first-fit of one 64-entry window against the node's
 // remaining capacity `rem` (wave-uniform), in lane (= rank) order.
-template <int D>
-__device__ __forceinline__ void decide_window(const Win<D> &wc, int64_t (&rem)[D],
-                                              int64_t (&add)[D], int lane, int node,
-                                              const AcceptOut &o) {
+template <int D, bool N32>
+__device__ __forceinline__ void decide_window(const Win<D, N32> &wc,
+                                              typename Win<D, N32>::NT (&rem)[D],
+                                              typename Win<D, N32>::NT (&add)[D], int lane,
+                                              int node, const AcceptOut &o) {
+  using NT = typename Win<D, N32>::NT;
   bool undecided = wc.m > 0, accepted = false;
   while (true) {
     bool fa = undecided;
@@ -482,24 +535,24 @@ __device__ __forceinline__ void decide_window(const Win<D> &wc, int64_t (&rem)[D
     // window is done without any prefix scan
     if (__ballot(fa) == 0) break;
     bool okp = fa;
-    int64_t pre[D];
+    NT pre[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      const int64_t x = fa ? wc.need[d] : 0;
-      pre[d] = wave_incl_scan_i64(x) - x;  // exclusive
-      okp &= pre[d] + wc.need[d] <= rem[d];
+      const NT x = fa ? wc.need[d] : 0;
+      pre[d] = scan_excl<N32>(x);
+      okp &= pre[d] <= rem[d] - wc.need[d];  // fa: need <= rem, no wrap
     }
     const uint64_t failm = __ballot(fa && !okp);
     if (failm == 0) {
       accepted |= fa;
 #pragma unroll
-      for (int d = 0; d < D; ++d) rem[d] -= readlane_i64(pre[d] + (fa ? wc.need[d] : 0), 63);
+      for (int d = 0; d < D; ++d) rem[d] -= readlane_nt((NT)(pre[d] + (fa ? wc.need[d] : 0)), 63);
       break;
     }
     const int f = __ffsll((unsigned long long)failm) - 1;
     accepted |= fa && lane < f;
 #pragma unroll
-    for (int d = 0; d < D; ++d) rem[d] -= readlane_i64(pre[d], f);
+    for (int d = 0; d < D; ++d) rem[d] -= readlane_nt(pre[d], f);
     undecided = fa && lane >= f;  // lane f is rejected on the next check
   }
   if (wc.m > 0 && accepted) {
@@ -540,8 +593,9 @@ struct AccArgs {
 // smallest request no longer fits the node's remaining capacity in some dim
 // are skipped unread (a contested node fills after a few windows; the rest of
 // its long bidder row is then rejected without loading it).
-template <int D>
+template <int D, bool N32>
 __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int node) {
+  using NT = typename Win<D, N32>::NT;
   const int lane = threadIdx.x & 63;
   const int N = ac.sp.N;
   const AcceptOut &o = ac.o;
@@ -554,10 +608,10 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
 #endif
   const int32_t e0 = ac.seg_start[node];
   const int32_t e1 = ac.seg_end[node];
-  int64_t rem[D], add[D];
+  NT rem[D], add[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    rem[d] = ac.cap[(int64_t)d * N + node] - o.used[(int64_t)d * N + node];
+    rem[d] = (NT)(ac.cap[(int64_t)d * N + node] - o.used[(int64_t)d * N + node]);
     add[d] = 0;
   }
   KP_PP_MARK(0);
@@ -577,7 +631,7 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
     while (true) {
       bool can = true;
 #pragma unroll
-      for (int d = 0; d < D; ++d) can &= wmin[d] <= rem[d];
+      for (int d = 0; d < D; ++d) can &= wmin[d] <= (int64_t)rem[d];
       flagged &= __ballot(can);
       if (!flagged) break;
       int wl[BATCH];
@@ -586,16 +640,16 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
         wl[t] = flagged ? wb + __ffsll((unsigned long long)flagged) - 1 : -1;
         flagged &= flagged ? flagged - 1 : 0;
       }
-      Win<D> wv[BATCH];
+      Win<D, N32> wv[BATCH];
 #pragma unroll
       for (int t = 0; t < BATCH; ++t)
-        load_win<D>(wv[t], wl[t], lane, e0, e1, pass, ac.P, ac.bid, ac.ent_q, ac.ent_unit,
+        load_win<D, N32>(wv[t], wl[t], lane, e0, e1, pass, ac.P, ac.bid, ac.ent_q, ac.ent_unit,
                     ac.ent_size, ac.ent_lead, ac.ent_slot, ac.s0);
       KP_PP_MARK(2);
 #pragma unroll
       for (int t = 0; t < BATCH; ++t) {
         if (wl[t] < 0) break;
-        decide_window<D>(wv[t], rem, add, lane, node, o);
+        decide_window<D, N32>(wv[t], rem, add, lane, node, o);
       }
       KP_PP_MARK(3);
     }
@@ -603,7 +657,7 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
   // fold the single-node units committed by this wave into `used`
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    const int64_t tot = readlane_i64(wave_incl_scan_i64(add[d]), 63);
+    const int64_t tot = (int64_t)readlane_nt((NT)(scan_excl<N32>(add[d]) + add[d]), 63);
     if (lane == 63 && tot != 0)
       atomicAdd(reinterpret_cast<unsigned long long *>(&o.used[(int64_t)d * N + node]),
                 (unsigned long long)tot);
@@ -612,7 +666,7 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
 
 // One wave per node: the nodes with bidders this round (use_list, small
 // rounds) or every node; nothing to do after a pass without proposals.
-template <int D>
+template <int D, bool N32>
 __global__ __launch_bounds__(256) void k_accept(AccArgs ac, int32_t pass, int32_t use_list) {
   const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int32_t pf = ac.pass_flag[pass];
@@ -624,7 +678,14 @@ __global__ __launch_bounds__(256) void k_accept(AccArgs ac, int32_t pass, int32_
   } else if (node >= ac.sp.N || !pf) {
     return;
   }
-  accept_node<D>(ac, pass, node);
+  accept_node<D, N32>(ac, pass, node);
+}
+
+// the W32 member loop's key: largest score + 64 * w_spread + 1 < 2^(32 - lb)
+static bool plan_key_ok(const ScoreParams &sp, int lb) {
+  int64_t bound = (int64_t)sp.w_gpu_fit + sp.w_affinity + 64 * (int64_t)sp.w_spread + 1;
+  for (int d = 0; d < sp.D; ++d) bound += (int64_t)sp.w[d] * sp.S;
+  return bound < ((int64_t)1 << (32 - lb));
 }
 
 static PlanArgs plan_args(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass,
@@ -657,6 +718,7 @@ static PlanArgs plan_args(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t p
   pa.nparts = c->d.nparts;
   pa.arrive = c->d.arrive;
   pa.node_flag = c->d.node_flag;
+  pa.key_off = (uint32_t)(64 * sp.w_spread + 1);
   pa.pp = c->d.fz_prof ? c->d.fz_prof + 16 : nullptr;
   pa.st = c->d.stats;
   return pa;
@@ -706,14 +768,16 @@ struct PlanL {
   static int run(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass,
                  const int32_t *A_dev) {
     const PlanArgs pa = plan_args(c, sp, A, pass, A_dev);
-    // 32-bit member loop whenever every cap and request < 2^32 (fits32)
+    // 32-bit member loop whenever every cap and request < 2^32 (fits32) and
+    // the packed (value, lane) key of the group max fits 32 bits
+    const bool w32 = c->fits32 && plan_key_ok(sp, sp.n_cand <= 16 ? 4 : 5);
     if (sp.n_cand <= 16) {
-      if (c->fits32)
+      if (w32)
         hipLaunchKernelGGL((k_plan<D, 16, true>), dim3(blocks(A, 4 * 4)), dim3(256), 0, c->stream, pa);
       else
         hipLaunchKernelGGL((k_plan<D, 16, false>), dim3(blocks(A, 4 * 4)), dim3(256), 0, c->stream, pa);
     } else {
-      if (c->fits32)
+      if (w32)
         hipLaunchKernelGGL((k_plan<D, 32, true>), dim3(blocks(A, 4 * 2)), dim3(256), 0, c->stream, pa);
       else
         hipLaunchKernelGGL((k_plan<D, 32, false>), dim3(blocks(A, 4 * 2)), dim3(256), 0, c->stream, pa);
@@ -730,8 +794,13 @@ struct AcceptL {
     // rounds with fewer bidder entries than nodes walk the active-node list
     const int32_t use_list = P < c->N || c->acc_list == 1 ? 1 : 0;
     const int64_t waves = std::min<int64_t>(P, c->N);
-    hipLaunchKernelGGL((k_accept<D>), dim3(blocks(waves, 4)), dim3(256), 0, c->stream, ac, pass,
-                       use_list);
+    // 32-bit first-fit sums while every capacity < 2^26 (64 terms stay < 2^32)
+    if (c->fits32 && c->max_cap < ((int64_t)1 << 26))
+      hipLaunchKernelGGL((k_accept<D, true>), dim3(blocks(waves, 4)), dim3(256), 0, c->stream, ac,
+                         pass, use_list);
+    else
+      hipLaunchKernelGGL((k_accept<D, false>), dim3(blocks(waves, 4)), dim3(256), 0, c->stream, ac,
+                         pass, use_list);
     KP_HIP(hipGetLastError());
     return KP_OK;
   }
