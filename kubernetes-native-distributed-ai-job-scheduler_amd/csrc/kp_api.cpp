@@ -128,6 +128,7 @@ static int ensure_nodes(kp_ctx *c, int32_t N, int32_t D) {
   KP_TRY(dalloc(&c->d.node_flag, (size_t)n));
   // +4: k_accept's list mode reads node_list[wave] for up to 3 padding waves
   KP_TRY(dalloc(&c->d.node_list, (size_t)n + 4));
+  KP_TRY(dalloc(&c->d.nrec, (size_t)n + 4));
   KP_TRY(dalloc(&c->d.perm, (size_t)n));
   c->cap_N = n;
   return KP_OK;
@@ -329,6 +330,7 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = std::getenv("KP_COMPACT_MAX")) c->compact_max = std::atoi(e);
   if (const char *e = std::getenv("KP_FUSED")) c->fused_enabled = std::atoi(e) != 0;
   if (const char *e = std::getenv("KP_ACC_LIST")) c->acc_list = std::atoi(e);
+  if (const char *e = std::getenv("KP_ACC_WAVES")) c->acc_waves = std::max(0, std::atoi(e));
   if (const char *e = std::getenv("KP_FZ_WG_TARGET")) c->fz_wg_target = std::max(64, std::atoi(e));
   if (const char *e = std::getenv("KP_COUNT_DIRECT")) c->count_direct = std::atoi(e) != 0;
   if (const char *e = std::getenv("KP_HOST_PROF")) c->host_prof = std::atoi(e) != 0;
@@ -661,7 +663,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
                           d.act, d.act_local, d.cand, d.cand_local, d.open, d.flag, d.s0, d.bid,
                           d.win, d.winmin, d.gpart, d.nparts, d.arrive, d.inv, d.ent_unit,
                           d.ent_slot, d.ent_size, d.ent_lead, d.ent_q, d.csr_kin, d.csr_vin,
-                          d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.node_flag, d.node_list,
+                          d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.node_flag, d.node_list, d.nrec,
                           d.pass_flag, d.counters, d.stats, d.temp};
     for (const void *ptr : need)
       if (!ptr) return fail(KP_ENOMEM, "kp_solve: a device buffer is missing");
@@ -1084,7 +1086,7 @@ void kp_destroy(kp_ctx *c) {
                   d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
                   d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.roff,
                   d.rreq, d.rsuf, d.rprio, d.pre_node, d.pre_vict, d.pre_cost,
-                  d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.stats, d.np32, d.colnode, d.wshift, d.part, d.fz_prof};
+                  d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.nrec, d.stats, d.np32, d.colnode, d.wshift, d.part, d.fz_prof};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->world > 1) {

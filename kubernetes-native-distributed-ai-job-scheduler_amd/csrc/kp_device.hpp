@@ -363,6 +363,32 @@ __device__ __forceinline__ int32_t group_max_i32(int32_t v) {
   return __builtin_amdgcn_readlane(v, 63);
 }
 
+// inclusive prefix sum inside aligned groups of G lanes (DPP row shifts, no
+// LDS crossbar): row_shr 1/2/4/8, then row_bcast 15 / 31 for G = 32 / 64
+template <int G>
+__device__ __forceinline__ int32_t group_incl_scan_i32(int32_t v) {
+  static_assert(G == 16 || G == 32 || G == 64, "group size");
+  const int l = lane_id(), rl = l & 15;
+  int32_t t;
+  t = __builtin_amdgcn_mov_dpp(v, 0x111, 0xf, 0xf, false);
+  if (rl >= 1) v += t;
+  t = __builtin_amdgcn_mov_dpp(v, 0x112, 0xf, 0xf, false);
+  if (rl >= 2) v += t;
+  t = __builtin_amdgcn_mov_dpp(v, 0x114, 0xf, 0xf, false);
+  if (rl >= 4) v += t;
+  t = __builtin_amdgcn_mov_dpp(v, 0x118, 0xf, 0xf, false);
+  if (rl >= 8) v += t;
+  if constexpr (G >= 32) {
+    t = __builtin_amdgcn_mov_dpp(v, 0x142, 0xf, 0xf, false);  // row_bcast:15
+    if ((l & 31) >= 16) v += t;
+  }
+  if constexpr (G >= 64) {
+    t = __builtin_amdgcn_mov_dpp(v, 0x143, 0xf, 0xf, false);  // row_bcast:31
+    if (l >= 32) v += t;
+  }
+  return v;
+}
+
 // u32 max over aligned groups of G lanes, returned to every lane of the
 // group: a DPP butterfly inside each 16-lane row (quad xor 1, quad xor 2,
 // half-row mirror, row mirror — each a max with a DPP operand), then the row

@@ -101,6 +101,7 @@ struct DevState {
   int32_t *seg_start = nullptr, *seg_end = nullptr;  // [N]
   int32_t *node_flag = nullptr; // [N] last pass in which the node received a bid
   int32_t *node_list = nullptr; // [N] nodes with bidders this round (count: counters[32])
+  int4 *nrec = nullptr;         // [N] per node_list entry {node, seg_start, seg_end, 0} (plan pass 0)
   int32_t *pass_flag = nullptr; // [64] pass p produced proposals
   // preemption: unit priorities, victim-pool CSR sorted
   // (node, prio desc, running index asc) with per-node suffix sums, outputs
@@ -157,6 +158,7 @@ struct kp_ctx {
   int32_t fz_wg_target = 2048;  // KP_FZ_WG_TARGET: target workgroups of k_score_topk
   bool fz_h16 = true;     // KP_FZ_H16=0: 32-bit LDS scores in k_score_topk
   int32_t fz_tie_bits = 0;  // KP_FZ_TIE_BITS=b (tests): b select-phase tie bits, forces collisions
+  int32_t acc_waves = 0;  // KP_ACC_WAVES: largest k_accept grid in waves (0 = one per node)
   int32_t acc_list = 1;  // KP_ACC_LIST=0: k_accept walks every node while entries >= nodes
   // KP_COMPACT_MAX: largest unit range compacted by the one-workgroup kernel
   int32_t compact_max = 262144;

@@ -31,6 +31,24 @@
 #include "kp_device.hpp"
 #include "kp_internal.hpp"
 
+#ifndef KP_ACC_BATCH
+#define KP_ACC_BATCH 2  // k_accept: flagged windows loaded together (2 < 4 < 8, tools/ab_mix.sh)
+#endif
+#ifndef KP_ACC_SPEC
+#define KP_ACC_SPEC 0  // 1: a bidder row's first loads issued before the node's pass flag is known (slower, tools/ab_mix.sh)
+#endif
+#ifndef KP_NREC
+#define KP_NREC 1  // plan pass 0 writes {node, seg_start, seg_end} records for accept
+#endif
+#ifndef KP_ACC_FAST1
+#define KP_ACC_FAST1 1  // one-window bidder rows skip the window-flag step
+#endif
+#ifndef KP_GANG_POST
+#define KP_GANG_POST 0  // >0: no prefetch; the last arriver loads this many parts at once
+#endif
+#ifndef KP_GANG_PRE
+#define KP_GANG_PRE 8  // gang parts prefetched with the arrival ticket (4: +1.4 ms, 8: -0.8 ms vs none)
+#endif
 #ifndef KP_ACC_FLAG_FIRST
 #define KP_ACC_FLAG_FIRST 0
 #endif
@@ -218,6 +236,9 @@ struct PlanArgs {
   int32_t *win, *s0_out, *pass_flag;
   int4 *gpart;
   int32_t *nparts, *arrive, *node_flag;
+  // pass 0 also writes the round's node records for accept (list mode)
+  const int32_t *node_list, *nl_count, *seg_start, *seg_end;
+  int4 *nrec;
   uint32_t key_off;        // W32 member loop: 64 * w_spread + 1 (plan_key_ok)
   uint64_t *pp;            // KP_PASS_PROFILE only
   const SolveStats *st;    // KP_PASS_PROFILE only (round index)
@@ -384,12 +405,7 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
   const uint64_t pm = (__ballot(prop) >> gbase) & GMASK;
   const int np = __popcll(pm);
   // member offset of this part = members of the earlier candidates
-  int32_t inc = planned;
-#pragma unroll
-  for (int d = 1; d < G; d <<= 1) {
-    const int32_t o = __shfl_up(inc, d, G);
-    if (gl >= d) inc += o;
-  }
+  const int32_t inc = group_incl_scan_i32<G>(planned);
   if (!slot_ok) return;
   if (fail) {
     if (gl == 0) {
@@ -399,7 +415,8 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
     return;
   }
   if (prop) {
-    pa.bid[e_inv] = ((uint32_t)pass << 8) | (uint32_t)planned;
+    // bid tag: pass << 16 | parts << 8 | members (parts <= K <= 32, members <= 64)
+    pa.bid[e_inv] = ((uint32_t)pass << 16) | ((uint32_t)np << 8) | (uint32_t)planned;
     pa.s0_out[e_inv] = s0;
     pa.win[e_inv >> 6] = pass;
     pa.node_flag[node] = pass;
@@ -419,6 +436,15 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
 
 template <int D, int G, bool W32>
 __global__ __launch_bounds__(256) void k_plan(PlanArgs pa) {
+  if (KP_NREC && pa.pass == 0) {
+    // the round's node records {node, seg_start, seg_end}: accept then finds
+    // a node's bidder row with its first load (one thread per list entry; the
+    // grid has >= A*K >= list-count threads)
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int32_t cnt = *pa.nl_count;
+    const int32_t n = i < pa.sp.N ? pa.node_list[i] : 0;
+    if (i < cnt) pa.nrec[i] = make_int4(n, pa.seg_start[n], pa.seg_end[n], 0);
+  }
   plan_wave<D, G, W32>(pa, pa.pass, blockIdx.x * 4 + (threadIdx.x >> 6));
 }
 
@@ -435,7 +461,7 @@ __global__ __launch_bounds__(256) void k_plan(PlanArgs pa) {
 template <int D, bool N32>
 struct Win {
   using NT = typename std::conditional<N32, uint32_t, int64_t>::type;
-  int32_t e, m, unit, size, lead, slot, s0;
+  int32_t e, m, np, unit, size, lead, slot, s0;
   NT need[D];
 };
 
@@ -451,6 +477,7 @@ __device__ __forceinline__ void load_win(Win<D, N32> &w, int wi, int lane, int32
                                          const int32_t *__restrict__ s0) {
   w.e = (wi << 6) + lane;
   w.m = 0;
+  w.np = 0;
   const bool in_row = wi >= 0 && w.e >= e0 && w.e < e1;
   const int32_t ee = in_row ? w.e : e0;
   const uint32_t t = bid[ee];
@@ -462,7 +489,10 @@ __device__ __forceinline__ void load_win(Win<D, N32> &w, int wi, int lane, int32
   int64_t qd[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) qd[d] = ent_q[(int64_t)d * P + ee];
-  if (in_row && (t >> 8) == (uint32_t)pass) w.m = (int32_t)(t & 0xFFu);
+  if (in_row && (t >> 16) == (uint32_t)pass) {
+    w.m = (int32_t)(t & 0xFFu);
+    w.np = (int32_t)((t >> 8) & 0xFFu);
+  }
   // a bid's members fit the node at plan time: m·q <= cap (< 2^26 with N32)
 #pragma unroll
   for (int d = 0; d < D; ++d)
@@ -483,24 +513,31 @@ struct AcceptOut {
 // all-or-nothing commit of a multi-node gang by the wave that accepted its
 // last part: every part's members go to the part's node, usage is added with
 // int64 atomics (other node waves may be folding into the same words)
+constexpr int kGangPre = KP_GANG_PRE;  // parts loaded together with the arrival ticket
+constexpr int kGangPreN = kGangPre > 0 ? kGangPre : 1;
+
+template <int D>
+__device__ __forceinline__ void commit_part(const AcceptOut &o, int32_t lead, const int4 &g,
+                                            const int64_t (&qq)[D]) {
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (qq[d] != 0)
+      atomicAdd(reinterpret_cast<unsigned long long *>(&o.used[(int64_t)d * o.N + g.x]),
+                (unsigned long long)((int64_t)g.y * qq[d]));
+  for (int m = 0; m < g.y; ++m) {
+    o.job_node[lead + g.z + m] = g.x;
+    o.job_score[lead + g.z + m] = g.w;
+  }
+}
+
 template <int D>
 __device__ __forceinline__ void commit_gang(const AcceptOut &o, int32_t slot, int32_t unit,
-                                         int32_t lead, int32_t np) {
-  int64_t qq[D];
+                                         int32_t lead, int32_t np, const int4 (&pre)[kGangPreN],
+                                         const int64_t (&qq)[D]) {
 #pragma unroll
-  for (int d = 0; d < D; ++d) qq[d] = o.q[(int64_t)d * o.U + unit];
-  for (int i = 0; i < np; ++i) {
-    const int4 g = o.gpart[(int64_t)slot * o.K + i];
-#pragma unroll
-    for (int d = 0; d < D; ++d)
-      if (qq[d] != 0)
-        atomicAdd(reinterpret_cast<unsigned long long *>(&o.used[(int64_t)d * o.N + g.x]),
-                  (unsigned long long)((int64_t)g.y * qq[d]));
-    for (int m = 0; m < g.y; ++m) {
-      o.job_node[lead + g.z + m] = g.x;
-      o.job_score[lead + g.z + m] = g.w;
-    }
-  }
+  for (int i = 0; i < kGangPre; ++i)  // static indices: the parts stay in registers
+    if (i < np) commit_part<D>(o, lead, pre[i], qq);
+  for (int i = kGangPre; i < np; ++i) commit_part<D>(o, lead, o.gpart[(int64_t)slot * o.K + i], qq);
   o.status[unit] = kPlaced;
   o.open[slot] = 0;
 }
@@ -565,9 +602,34 @@ __device__ __forceinline__ void decide_window(const Win<D, N32> &wc,
       o.open[wc.slot] = 0;
 #pragma unroll
       for (int d = 0; d < D; ++d) add[d] += wc.need[d];
-    } else {  // one part of a multi-node gang
-      const int32_t np = o.nparts[wc.slot];
-      if (atomicAdd(&o.arrive[wc.slot], 1) + 1 == np) commit_gang<D>(o, wc.slot, wc.unit, wc.lead, np);
+    } else {  // one part of a multi-node gang: the part count came with the bid
+      // the first parts and the request are loaded together with the arrival
+      // ticket, so the last arriver commits without another round trip
+      int4 pre[kGangPreN];
+#pragma unroll
+      for (int i = 0; i < kGangPre; ++i)
+        pre[i] = i < wc.np ? o.gpart[(int64_t)wc.slot * o.K + i] : make_int4(0, 0, 0, 0);
+      int64_t qq[D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) qq[d] = o.q[(int64_t)d * o.U + wc.unit];
+      if (atomicAdd(&o.arrive[wc.slot], 1) + 1 == wc.np) {
+#if KP_GANG_POST > 0
+        // the last arriver loads its gang's parts together (not one per part)
+        int4 post[KP_GANG_POST];
+#pragma unroll
+        for (int i = 0; i < KP_GANG_POST; ++i)
+          post[i] = i < wc.np ? o.gpart[(int64_t)wc.slot * o.K + i] : make_int4(0, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < KP_GANG_POST; ++i)
+          if (i < wc.np) commit_part<D>(o, wc.lead, post[i], qq);
+        for (int i = KP_GANG_POST; i < wc.np; ++i)
+          commit_part<D>(o, wc.lead, o.gpart[(int64_t)wc.slot * o.K + i], qq);
+        o.status[wc.unit] = kPlaced;
+        o.open[wc.slot] = 0;
+#else
+        commit_gang<D>(o, wc.slot, wc.unit, wc.lead, wc.np, pre, qq);
+#endif
+      }
     }
   }
 }
@@ -582,6 +644,7 @@ struct AccArgs {
   const int32_t *ent_unit, *ent_size, *ent_lead, *ent_slot;
   const int64_t *cap;
   const int32_t *node_flag, *node_list, *nl_count, *pass_flag;
+  const int4 *nrec;
   const int64_t *winmin;
   int64_t nwin;
   AcceptOut o;
@@ -589,12 +652,15 @@ struct AccArgs {
   const SolveStats *st;    // KP_PASS_PROFILE only (round index)
 };
 
-// the bidders of `node` in pass `pass` (whole wave). Flagged windows whose
-// smallest request no longer fits the node's remaining capacity in some dim
-// are skipped unread (a contested node fills after a few windows; the rest of
-// its long bidder row is then rejected without loading it).
+// the bidders of `node` (bidder row [e0, e1)) in pass `pass` (whole wave).
+// A one-window row is loaded together with the node's own operands (no
+// window flag); otherwise the window flags and smallest requests are, and
+// flagged windows whose smallest request no longer fits the node's remaining
+// capacity in some dim are skipped unread (a contested node fills after a
+// few windows; the rest of its long bidder row is then rejected unread).
 template <int D, bool N32>
-__device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int node) {
+__device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int node, int32_t e0,
+                                            int32_t e1) {
   using NT = typename Win<D, N32>::NT;
   const int lane = threadIdx.x & 63;
   const int N = ac.sp.N;
@@ -602,56 +668,68 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
 #ifdef KP_PASS_PROFILE
   KP_PP_DECL(ac.pp, 16, ac.pp ? (int)(ac.st->rounds - 1) * 16 + pass : 1024);
 #endif
+  if (e0 < 0) return;  // no bidder row this round
   const int32_t nf = ac.node_flag[node];
-#if KP_ACC_FLAG_FIRST  // A/B: test the node flag before loading the node's operands
-  if (nf != pass) return;
-#endif
-  const int32_t e0 = ac.seg_start[node];
-  const int32_t e1 = ac.seg_end[node];
   NT rem[D], add[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
     rem[d] = (NT)(ac.cap[(int64_t)d * N + node] - o.used[(int64_t)d * N + node]);
     add[d] = 0;
   }
-  KP_PP_MARK(0);
-  if (nf != pass || e0 < 0) return;  // nobody bid on this node in this pass
-  KP_PP_WORK();
   const int32_t w0 = e0 >> 6, w1 = (e1 - 1) >> 6;
-  constexpr int BATCH = 4;  // flagged windows whose operands are loaded together
-  for (int wb = w0; wb <= w1; wb += 64) {
-    // a one-window segment is loaded without consulting its window flag
-    const int wi = wb + lane;
-    const bool mine = wi <= w1;
-    int64_t wmin[D];
+#if !KP_ACC_SPEC
+  if (nf != pass) return;  // nobody bid on this node in this pass
+#endif
+  if (KP_ACC_FAST1 && w0 == w1) {
+    Win<D, N32> wv;
+    load_win<D, N32>(wv, w0, lane, e0, e1, pass, ac.P, ac.bid, ac.ent_q, ac.ent_unit, ac.ent_size,
+                     ac.ent_lead, ac.ent_slot, ac.s0);
+    KP_PP_MARK(0);
+    if (nf != pass) return;  // nobody bid on this node in this pass
+    KP_PP_WORK();
+    decide_window<D, N32>(wv, rem, add, lane, node, o);
+    KP_PP_MARK(3);
+  } else {
+    constexpr int BATCH = KP_ACC_BATCH;  // flagged windows whose operands are loaded together
+    for (int wb = w0; wb <= w1; wb += 64) {
+      const int wi = wb + lane;
+      const bool mine = wi <= w1;
+      int64_t wmin[D];
 #pragma unroll
-    for (int d = 0; d < D; ++d) wmin[d] = mine ? ac.winmin[(int64_t)d * ac.nwin + wi] : 0;
-    uint64_t flagged = w0 == w1 ? 1ull : __ballot(mine && ac.win[wi] == pass);
-    KP_PP_MARK(1);
-    while (true) {
-      bool can = true;
-#pragma unroll
-      for (int d = 0; d < D; ++d) can &= wmin[d] <= (int64_t)rem[d];
-      flagged &= __ballot(can);
-      if (!flagged) break;
-      int wl[BATCH];
-#pragma unroll
-      for (int t = 0; t < BATCH; ++t) {
-        wl[t] = flagged ? wb + __ffsll((unsigned long long)flagged) - 1 : -1;
-        flagged &= flagged ? flagged - 1 : 0;
+      for (int d = 0; d < D; ++d) wmin[d] = mine ? ac.winmin[(int64_t)d * ac.nwin + wi] : 0;
+      const int32_t wf = mine ? ac.win[wi] : -1;
+      if (wb == w0) {  // the first chunk's flags were loaded with the node's operands
+        KP_PP_MARK(0);
+        if (nf != pass) return;
+        KP_PP_WORK();
       }
-      Win<D, N32> wv[BATCH];
+      uint64_t flagged = __ballot(wf == pass);
+      KP_PP_MARK(1);
+      while (true) {
+        bool can = true;
 #pragma unroll
-      for (int t = 0; t < BATCH; ++t)
-        load_win<D, N32>(wv[t], wl[t], lane, e0, e1, pass, ac.P, ac.bid, ac.ent_q, ac.ent_unit,
-                    ac.ent_size, ac.ent_lead, ac.ent_slot, ac.s0);
-      KP_PP_MARK(2);
+        for (int d = 0; d < D; ++d) can &= wmin[d] <= (int64_t)rem[d];
+        flagged &= __ballot(can);
+        if (!flagged) break;
+        int wl[BATCH];
 #pragma unroll
-      for (int t = 0; t < BATCH; ++t) {
-        if (wl[t] < 0) break;
-        decide_window<D, N32>(wv[t], rem, add, lane, node, o);
+        for (int t = 0; t < BATCH; ++t) {
+          wl[t] = flagged ? wb + __ffsll((unsigned long long)flagged) - 1 : -1;
+          flagged &= flagged ? flagged - 1 : 0;
+        }
+        Win<D, N32> wv[BATCH];
+#pragma unroll
+        for (int t = 0; t < BATCH; ++t)
+          load_win<D, N32>(wv[t], wl[t], lane, e0, e1, pass, ac.P, ac.bid, ac.ent_q, ac.ent_unit,
+                           ac.ent_size, ac.ent_lead, ac.ent_slot, ac.s0);
+        KP_PP_MARK(2);
+#pragma unroll
+        for (int t = 0; t < BATCH; ++t) {
+          if (wl[t] < 0) break;
+          decide_window<D, N32>(wv[t], rem, add, lane, node, o);
+        }
+        KP_PP_MARK(3);
       }
-      KP_PP_MARK(3);
     }
   }
   // fold the single-node units committed by this wave into `used`
@@ -664,21 +742,39 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
   }
 }
 
-// One wave per node: the nodes with bidders this round (use_list, small
-// rounds) or every node; nothing to do after a pass without proposals.
+// One wave per node: the nodes with bidders this round (use_list: their
+// records {node, seg_start, seg_end}, written by plan pass 0) or every node;
+// nothing to do after a pass without proposals.
 template <int D, bool N32>
 __global__ __launch_bounds__(256) void k_accept(AccArgs ac, int32_t pass, int32_t use_list) {
   const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nw = gridDim.x * 4;  // grid-stride: the grid may be smaller than the node count
   const int32_t pf = ac.pass_flag[pass];
-  int node = wv;
-  if (use_list) {  // list entry and count loaded together (node_list has 4 spare entries)
+  if (use_list) {  // first record and count loaded together (nrec has 4 spare entries)
+#if KP_NREC
+    const int4 r = ac.nrec[wv];
+    const int32_t cnt = *ac.nl_count;
+    if (wv >= cnt || !pf) return;
+    accept_node<D, N32>(ac, pass, r.x, r.y, r.z);
+    for (int i = wv + nw; i < cnt; i += nw) {
+      const int4 ri = ac.nrec[i];
+      accept_node<D, N32>(ac, pass, ri.x, ri.y, ri.z);
+    }
+#else
     const int32_t nd = ac.node_list[wv];
-    if (wv >= *ac.nl_count || !pf) return;
-    node = nd;
-  } else if (node >= ac.sp.N || !pf) {
-    return;
+    const int32_t cnt = *ac.nl_count;
+    if (wv >= cnt || !pf) return;
+    accept_node<D, N32>(ac, pass, nd, ac.seg_start[nd], ac.seg_end[nd]);
+    for (int i = wv + nw; i < cnt; i += nw) {
+      const int32_t ni = ac.node_list[i];
+      accept_node<D, N32>(ac, pass, ni, ac.seg_start[ni], ac.seg_end[ni]);
+    }
+#endif
+  } else {
+    if (!pf) return;
+    for (int node = wv; node < ac.sp.N; node += nw)
+      accept_node<D, N32>(ac, pass, node, ac.seg_start[node], ac.seg_end[node]);
   }
-  accept_node<D, N32>(ac, pass, node);
 }
 
 // the W32 member loop's key: largest score + 64 * w_spread + 1 < 2^(32 - lb)
@@ -719,6 +815,11 @@ static PlanArgs plan_args(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t p
   pa.arrive = c->d.arrive;
   pa.node_flag = c->d.node_flag;
   pa.key_off = (uint32_t)(64 * sp.w_spread + 1);
+  pa.node_list = c->d.node_list;
+  pa.nl_count = c->d.counters + 32;
+  pa.seg_start = c->d.seg_start;
+  pa.seg_end = c->d.seg_end;
+  pa.nrec = c->d.nrec;
   pa.pp = c->d.fz_prof ? c->d.fz_prof + 16 : nullptr;
   pa.st = c->d.stats;
   return pa;
@@ -741,6 +842,7 @@ static AccArgs acc_args(kp_ctx *c, const ScoreParams &sp, int64_t P) {
   ac.cap = c->d.cap;
   ac.node_flag = c->d.node_flag;
   ac.node_list = c->d.node_list;
+  ac.nrec = c->d.nrec;
   ac.nl_count = c->d.counters + 32;
   ac.pass_flag = c->d.pass_flag;
   ac.winmin = c->d.winmin;
@@ -793,7 +895,10 @@ struct AcceptL {
     const AccArgs ac = acc_args(c, sp, P);
     // rounds with fewer bidder entries than nodes walk the active-node list
     const int32_t use_list = P < c->N || c->acc_list == 1 ? 1 : 0;
-    const int64_t waves = std::min<int64_t>(P, c->N);
+    // nodes with bidders <= min(P, N); KP_ACC_WAVES caps the grid (grid-stride
+    // loop over the rest): most of a late round's grid would only dispatch and exit
+    int64_t waves = std::min<int64_t>(P, c->N);
+    if (c->acc_waves > 0) waves = std::min<int64_t>(waves, c->acc_waves);
     // 32-bit first-fit sums while every capacity < 2^26 (64 terms stay < 2^32)
     if (c->fits32 && c->max_cap < ((int64_t)1 << 26))
       hipLaunchKernelGGL((k_accept<D, true>), dim3(blocks(waves, 4)), dim3(256), 0, c->stream, ac,
