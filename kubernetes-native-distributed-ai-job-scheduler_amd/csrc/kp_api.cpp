@@ -129,6 +129,7 @@ static int ensure_nodes(kp_ctx *c, int32_t N, int32_t D) {
   // +4: k_accept's list mode reads node_list[wave] for up to 3 padding waves
   KP_TRY(dalloc(&c->d.node_list, (size_t)n + 4));
   KP_TRY(dalloc(&c->d.nrec, (size_t)n + 4));
+  KP_TRY(dalloc(&c->d.nst, (size_t)n * 16));
   KP_TRY(dalloc(&c->d.perm, (size_t)n));
   c->cap_N = n;
   return KP_OK;
@@ -647,6 +648,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   const int32_t K = p->n_cand, U = c->U, N = c->N;
   const int64_t Ns = (N + 63) & ~63;
   KP_TRY(prep_for(c, p));
+  KP_TRY(launch_node_rec(c));
   // salts of the rotated tie-break
   {
     std::vector<uint32_t> salt(U);
@@ -663,7 +665,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
                           d.act, d.act_local, d.cand, d.cand_local, d.open, d.flag, d.s0, d.bid,
                           d.win, d.winmin, d.gpart, d.nparts, d.arrive, d.inv, d.ent_unit,
                           d.ent_slot, d.ent_size, d.ent_lead, d.ent_q, d.csr_kin, d.csr_vin,
-                          d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.node_flag, d.node_list, d.nrec,
+                          d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.node_flag, d.node_list, d.nrec, d.nst,
                           d.pass_flag, d.counters, d.stats, d.temp};
     for (const void *ptr : need)
       if (!ptr) return fail(KP_ENOMEM, "kp_solve: a device buffer is missing");
@@ -1086,7 +1088,7 @@ void kp_destroy(kp_ctx *c) {
                   d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
                   d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.roff,
                   d.rreq, d.rsuf, d.rprio, d.pre_node, d.pre_vict, d.pre_cost,
-                  d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.nrec, d.stats, d.np32, d.colnode, d.wshift, d.part, d.fz_prof};
+                  d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.nrec, d.nst, d.stats, d.np32, d.colnode, d.wshift, d.part, d.fz_prof};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->world > 1) {

@@ -101,7 +101,8 @@ struct DevState {
   int32_t *seg_start = nullptr, *seg_end = nullptr;  // [N]
   int32_t *node_flag = nullptr; // [N] last pass in which the node received a bid
   int32_t *node_list = nullptr; // [N] nodes with bidders this round (count: counters[32])
-  int4 *nrec = nullptr;         // [N] per node_list entry {node, seg_start, seg_end, 0} (plan pass 0)
+  int4 *nrec = nullptr;
+  uint32_t *nst = nullptr;      // [N][16] static plan record (D <= 4, fits32): cap, R, K per dim, base, topo         // [N] per node_list entry {node, seg_start, seg_end, 0} (plan pass 0)
   int32_t *pass_flag = nullptr; // [64] pass p produced proposals
   // preemption: unit priorities, victim-pool CSR sorted
   // (node, prio desc, running index asc) with per-node suffix sums, outputs
@@ -237,6 +238,8 @@ int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass,
 int launch_active_async(kp_ctx *c, int32_t lo, int32_t hi, int32_t *count_host,
                         bool *direct = nullptr);
 int launch_accept(kp_ctx *c, const ScoreParams &sp, int32_t pass, int32_t A);
+// the static per-node plan records d.nst (every solve, after the division tables)
+int launch_node_rec(kp_ctx *c);
 void launch_probe(kp_ctx *c, const ScoreParams &sp, int32_t A);
 int launch_active(kp_ctx *c, int32_t lo, int32_t hi, int32_t *A_host);
 int launch_reset_units(kp_ctx *c);

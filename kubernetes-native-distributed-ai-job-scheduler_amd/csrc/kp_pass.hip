@@ -239,6 +239,7 @@ struct PlanArgs {
   // pass 0 also writes the round's node records for accept (list mode)
   const int32_t *node_list, *nl_count, *seg_start, *seg_end;
   int4 *nrec;
+  const uint32_t *nst;
   uint32_t key_off;        // W32 member loop: 64 * w_spread + 1 (plan_key_ok)
   uint64_t *pp;            // KP_PASS_PROFILE only
   const SolveStats *st;    // KP_PASS_PROFILE only (round index)
@@ -285,7 +286,27 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
   const int nn = valid ? node : 0;
   int32_t planned = 0, dom = 0, s0 = -1;
   bool fail = !slot_ok;
-  const int32_t tp = pa.topo[nn];
+  // this lane's candidate node: the static operands of the W32 loop come as
+  // one 64-byte record (D <= 4) instead of 3D + 2 separate gathers
+  constexpr bool REC = W32 && D <= 4;
+  uint32_t ncap[D], nR[D], nK[D];
+  int32_t nbase = 0, tp;
+  if constexpr (REC) {
+    const uint4 *rec = reinterpret_cast<const uint4 *>(pa.nst) + (int64_t)nn * 4;
+    const uint4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
+    const uint32_t c4[4] = {r0.x, r0.y, r0.z, r0.w}, R4[4] = {r1.x, r1.y, r1.z, r1.w},
+                   K4[4] = {r2.x, r2.y, r2.z, r2.w};
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      ncap[d] = c4[d];
+      nR[d] = R4[d];
+      nK[d] = K4[d];
+    }
+    nbase = (int32_t)r3.x;
+    tp = (int32_t)r3.y;
+  } else {
+    tp = pa.topo[nn];
+  }
   int32_t szmax = sz;
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) szmax = max(szmax, __shfl_xor(szmax, m, kWave));
@@ -301,8 +322,9 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
     for (int d = 0; d < D; ++d) {
       q32[d] = (uint32_t)qq[d];
       const uint32_t uu = (uint32_t)pa.used[(int64_t)d * N + nn];
-      const uint32_t cc = (uint32_t)pa.cap[(int64_t)d * N + nn];
-      const uint32_t rr = pa.R32[(int64_t)d * N + nn], kk = pa.K32[(int64_t)d * N + nn];
+      const uint32_t cc = REC ? ncap[d] : (uint32_t)pa.cap[(int64_t)d * N + nn];
+      const uint32_t rr = REC ? nR[d] : pa.R32[(int64_t)d * N + nn];
+      const uint32_t kk = REC ? nK[d] : pa.K32[(int64_t)d * N + nn];
       rem[d] = cc - uu;
       // garbage (never used) on a lane where q does not fit: x = u + q may wrap
       divmod32(uu + q32[d], cc, rr, kk, (uint32_t)sp.S, t_[d], r_[d]);
@@ -310,7 +332,7 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
       // c = 0 (then q = 0 on a feasible lane): the dim stays 0, never wraps
       thr[d] = cc ? cc - rho[d] : 0xFFFFFFFFu;
     }
-    const int32_t b = (int32_t)pa.base[nn];
+    const int32_t b = REC ? nbase : (int32_t)pa.base[nn];
     const int g = sp.gpu_dim;
     const int32_t abonus = (af >= 0 && tp == af) ? sp.w_affinity : 0;
     // Σ_d w_d·t_d, stepped with the utilisations (w_d·Q_d precomputed)
@@ -820,6 +842,7 @@ static PlanArgs plan_args(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t p
   pa.seg_start = c->d.seg_start;
   pa.seg_end = c->d.seg_end;
   pa.nrec = c->d.nrec;
+  pa.nst = c->d.nst;
   pa.pp = c->d.fz_prof ? c->d.fz_prof + 16 : nullptr;
   pa.st = c->d.stats;
   return pa;
@@ -973,6 +996,36 @@ int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass, const
 int launch_accept(kp_ctx *c, const ScoreParams &sp, int32_t pass, int32_t A) {
   if (c->N <= 0 || A <= 0) return KP_OK;
   return dispatch_D<AcceptL>(c->D, c, sp, pass, (int64_t)A * sp.n_cand);
+}
+
+__global__ void k_node_rec(int32_t N, int32_t D, const int64_t *__restrict__ cap,
+                           const uint32_t *__restrict__ R32, const uint32_t *__restrict__ K32,
+                           const int64_t *__restrict__ base, const int32_t *__restrict__ topo,
+                           uint4 *__restrict__ nst) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  uint32_t w[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int d = 0; d < D; ++d) {
+    w[d] = (uint32_t)cap[(int64_t)d * N + n];
+    w[4 + d] = R32[(int64_t)d * N + n];
+    w[8 + d] = K32[(int64_t)d * N + n];
+  }
+  w[12] = (uint32_t)base[n];
+  w[13] = (uint32_t)topo[n];
+  uint4 *r = nst + (int64_t)n * 4;
+  r[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  r[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  r[2] = make_uint4(w[8], w[9], w[10], w[11]);
+  r[3] = make_uint4(w[12], w[13], 0u, 0u);
+}
+
+int launch_node_rec(kp_ctx *c) {
+  if (c->N <= 0 || c->D > 4 || !c->fits32) return KP_OK;  // the plan's REC form only
+  hipLaunchKernelGGL(k_node_rec, dim3(blocks(c->N, 256)), dim3(256), 0, c->stream, c->N, c->D,
+                     c->d.cap, c->d.R32, c->d.K32, c->d.base, c->d.topo,
+                     reinterpret_cast<uint4 *>(c->d.nst));
+  KP_HIP(hipGetLastError());
+  return KP_OK;
 }
 
 // KP_HOST_PROF probe: GPU time per launch of dependent no-op launches on the
