@@ -331,6 +331,8 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = std::getenv("KP_COMPACT_MAX")) c->compact_max = std::atoi(e);
   if (const char *e = std::getenv("KP_FUSED")) c->fused_enabled = std::atoi(e) != 0;
   if (const char *e = std::getenv("KP_ACC_LIST")) c->acc_list = std::atoi(e);
+  if (const char *e = std::getenv("KP_CSR_SORT")) c->csr_count_enabled = std::atoi(e) == 0;
+  if (const char *e = std::getenv("KP_CSR_BM_MAX")) c->csr_bm_max = std::atoll(e);
   if (const char *e = std::getenv("KP_ACC_WAVES")) c->acc_waves = std::max(0, std::atoi(e));
   if (const char *e = std::getenv("KP_FZ_WG_TARGET")) c->fz_wg_target = std::max(64, std::atoi(e));
   if (const char *e = std::getenv("KP_COUNT_DIRECT")) c->count_direct = std::atoi(e) != 0;
@@ -1088,7 +1090,8 @@ void kp_destroy(kp_ctx *c) {
                   d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
                   d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.roff,
                   d.rreq, d.rsuf, d.rprio, d.pre_node, d.pre_vict, d.pre_cost,
-                  d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.nrec, d.nst, d.stats, d.np32, d.colnode, d.wshift, d.part, d.fz_prof};
+                  d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.nrec, d.nst, d.stats, d.np32, d.colnode, d.wshift, d.part, d.fz_prof,
+                  d.bm, d.rowinfo, d.cnt};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->world > 1) {

@@ -119,6 +119,11 @@ struct DevState {
   int32_t *dl_bad = nullptr;    // [16] violation flag (allocated at kp_create)
   int32_t *counters = nullptr;  // small device counters
   SolveStats *stats = nullptr;  // [1]
+  // counting-mode CSR (kp_pass.hip): [N][ceil(A/32)] slot bitmap (all-zero
+  // between rounds), per word {rank of its first bit in the row, bits}, row lengths
+  uint32_t *bm = nullptr;
+  uint2 *rowinfo = nullptr;
+  int32_t *cnt = nullptr;
   void *temp = nullptr;         // rocprim temporary storage
   size_t temp_bytes = 0;
   // dist exchange
@@ -163,6 +168,14 @@ struct kp_ctx {
   int32_t acc_list = 1;  // KP_ACC_LIST=0: k_accept walks every node while entries >= nodes
   // KP_COMPACT_MAX: largest unit range compacted by the one-workgroup kernel
   int32_t compact_max = 262144;
+  // node -> bidder index by counting (KP_CSR_SORT=1: rocprim radix sort)
+  bool csr_count_enabled = true, bm_dirty = false;
+  int32_t csr_mode = 0;  // the current round's index: 1 counting, 0 sort
+  // counting mode while the round's bitmap (N x ceil(A/32) words) has at most
+  // this many words (KP_CSR_BM_MAX); larger rounds use the radix sort
+  int64_t csr_bm_max = int64_t{1} << 25;
+  int64_t cap_bm_words = 0;
+  int32_t cap_cnt_N = 0;
   // sizes
   int32_t N = 0, D = 0, J = 0, U = 0, R = 0, cap_R = 0, cap_delta = 0;
   int32_t cap_N = 0, cap_U = 0, cap_J = 0, cap_rows = 0, cap_props = 0, cap_K = 0;

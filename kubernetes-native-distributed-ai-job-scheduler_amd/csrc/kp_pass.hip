@@ -134,7 +134,8 @@ __global__ void k_csr_keys(int32_t A, int32_t K, int32_t N, int64_t nwin,
                            int32_t *__restrict__ pass_flag, int32_t *__restrict__ node_flag,
                            int32_t *__restrict__ nl_count, const int32_t *__restrict__ A_dev,
                            SolveStats *__restrict__ st, const int32_t *__restrict__ act,
-                           uint8_t *__restrict__ open, int32_t *__restrict__ status) {
+                           uint8_t *__restrict__ open, int32_t *__restrict__ status,
+                           uint32_t *__restrict__ bm, int64_t Wb) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int32_t Aa = A_dev ? min(A, *A_dev) : A;  // slots past the device count: no bids
   if (t == 0 && Aa > 0) {  // one writer: a round with active units
@@ -149,8 +150,12 @@ __global__ void k_csr_keys(int32_t A, int32_t K, int32_t N, int64_t nwin,
   if (t < (int64_t)A * K) {
     const int32_t n = t < (int64_t)Aa * K ? cand[t] : -1;
     const int32_t a = (int32_t)(t / K), c = (int32_t)(t % K);
-    keys[t] = n >= 0 ? (uint32_t)n : (uint32_t)N;  // invalid entries sort after every node
-    vals[t] = ((uint32_t)a << 5) | (uint32_t)c;     // K <= 32
+    if (bm) {  // counting mode: slot a bids on node n = bit a of row n
+      if (n >= 0) atomicOr(&bm[(int64_t)n * Wb + (a >> 5)], 1u << (a & 31));
+    } else {
+      keys[t] = n >= 0 ? (uint32_t)n : (uint32_t)N;  // invalid entries sort after every node
+      vals[t] = ((uint32_t)a << 5) | (uint32_t)c;     // K <= 32
+    }
     bid[t] = kNoBid;
   }
   if (t < N) {
@@ -212,6 +217,127 @@ __global__ void k_csr_finish(int32_t P, int32_t N, int32_t K, int32_t D, int32_t
   if (e == P - 1 || keys[e + 1] != k) seg_end[k] = e + 1;
 }
 
+// ---- node -> bidder index by counting (no sort) ----------------------------------
+// k_csr_keys sets bit a of row n of a [N][Wb] bitmap (Wb = ceil(A/32)) for
+// every candidate n of slot a. k_csr_rows (one wave per row) turns it into,
+// per nonzero word, {rank of the word's first set bit within the row, the
+// bits} and the row length, and clears the row; k_csr_scan (one workgroup)
+// scans the row lengths into node segments (node order). k_csr_place then
+// gives candidate (a, c) its entry e = segment start + rank of bit a, so each
+// node's bidder row is in slot (= rank) order: a stable counting sort keyed by
+// node id. (A last-workgroup-done scan inside k_csr_rows needs a device-scope
+// fence per wave: 150-280 us per launch measured, vs one more launch.)
+__global__ __launch_bounds__(1024) void k_csr_rows(int32_t N, int64_t Wb,
+                                                   uint32_t *__restrict__ bm,
+                                                   uint2 *__restrict__ rowinfo,
+                                                   int32_t *__restrict__ cnt) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 16 + (threadIdx.x >> 6);
+  if (n >= N) return;  // wave-uniform
+  const int64_t rb = (int64_t)n * Wb;
+  int32_t tot = 0;
+  for (int64_t w0 = 0; w0 < Wb; w0 += 256) {
+    uint32_t b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // four independent loads in flight
+      const int64_t w = w0 + i * 64 + lane;
+      b[i] = w < Wb ? bm[rb + w] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int32_t c = __popc(b[i]);
+      const int32_t inc = wave_incl_scan_i32(c);
+      if (b[i]) {
+        const int64_t w = w0 + i * 64 + lane;
+        rowinfo[rb + w] = make_uint2((uint32_t)(tot + inc - c), b[i]);
+        bm[rb + w] = 0u;  // the bitmap is all-zero between rounds
+      }
+      tot += __builtin_amdgcn_readlane(inc, 63);
+    }
+  }
+  if (lane == 0) cnt[n] = tot;
+}
+
+// one workgroup: row lengths -> node segments and the node list (node order).
+// (Staging the lengths through LDS in 16k-node tiles: 9 vs 7 us per launch.)
+__global__ __launch_bounds__(1024) void k_csr_scan(int32_t N, const int32_t *__restrict__ cnt,
+                                                   int32_t *__restrict__ seg_start,
+                                                   int32_t *__restrict__ seg_end,
+                                                   int32_t *__restrict__ node_list,
+                                                   int4 *__restrict__ nrec,
+                                                   int32_t *__restrict__ nl_count,
+                                                   int32_t *__restrict__ ptot) {
+  __shared__ int32_t s_sum[16], s_ne[16];
+  const int T = blockDim.x, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int per = (N + T - 1) / T;
+  const int lo = min(N, tid * per), hi = min(N, lo + per);
+  int32_t sum = 0, ne = 0;
+  for (int i = lo; i < hi; ++i) {
+    const int32_t v = cnt[i];
+    sum += v;
+    ne += v > 0 ? 1 : 0;
+  }
+  const int32_t isum = wave_incl_scan_i32(sum), ine = wave_incl_scan_i32(ne);
+  if (lane == 63) {
+    s_sum[wv] = isum;
+    s_ne[wv] = ine;
+  }
+  __syncthreads();
+  int32_t bsum = 0, bne = 0, tsum = 0, tne = 0;
+  for (int w = 0; w < T / 64; ++w) {
+    if (w < wv) {
+      bsum += s_sum[w];
+      bne += s_ne[w];
+    }
+    tsum += s_sum[w];
+    tne += s_ne[w];
+  }
+  int32_t e = bsum + isum - sum, k = bne + ine - ne;
+  for (int i = lo; i < hi; ++i) {
+    const int32_t v = cnt[i];
+    if (v > 0) {  // empty rows keep seg_start = -1 (k_csr_keys)
+      seg_start[i] = e;
+      seg_end[i] = e + v;
+      node_list[k] = i;
+      nrec[k] = make_int4(i, e, e + v, 0);
+      ++k;
+      e += v;
+    }
+  }
+  if (tid == 0) {
+    *nl_count = tne;
+    *ptot = tsum;
+  }
+}
+
+__global__ void k_csr_place(int32_t A, int32_t K, int32_t D, int32_t U, int64_t Wb, int64_t P,
+                            const int32_t *__restrict__ A_dev, const int32_t *__restrict__ cand,
+                            const int32_t *__restrict__ act, const int64_t *__restrict__ q,
+                            const int32_t *__restrict__ size, const int32_t *__restrict__ leader,
+                            const int32_t *__restrict__ seg_start,
+                            const uint2 *__restrict__ rowinfo, int32_t *__restrict__ inv,
+                            int32_t *__restrict__ ent_unit, int32_t *__restrict__ ent_slot,
+                            int32_t *__restrict__ ent_size, int32_t *__restrict__ ent_lead,
+                            int64_t *__restrict__ ent_q) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int32_t Aa = A_dev ? min(A, *A_dev) : A;
+  if (t >= (int64_t)Aa * K) return;
+  const int32_t n = cand[t];
+  const int32_t a = (int32_t)(t / K);
+  const int32_t u = act[a];
+  if (n < 0) return;
+  const int32_t ss = seg_start[n];
+  const uint2 ri = rowinfo[(int64_t)n * Wb + (a >> 5)];
+  const int32_t e = ss + (int32_t)ri.x + __popc(ri.y & ((1u << (a & 31)) - 1u));
+  inv[t] = e;
+  // operands of entry e in bidder order (k_accept's window loads)
+  ent_unit[e] = u;
+  ent_slot[e] = a;
+  ent_size[e] = size[u];
+  ent_lead[e] = leader[u];
+  for (int d = 0; d < D; ++d) ent_q[(int64_t)d * P + e] = q[(int64_t)d * U + u];
+}
+
 // ---- plan ------------------------------------------------------------------------
 // G lanes per slot (G >= K), 64/G slots per wave. Members are planned one at a
 // time: each lane scores its candidate with the members it already holds,
@@ -240,6 +366,13 @@ struct PlanArgs {
   const int32_t *node_list, *nl_count, *seg_start, *seg_end;
   int4 *nrec;
   const uint32_t *nst;
+  // counting-mode CSR (k_csr_rows / k_csr_place): pass 0 also computes the
+  // per-64-entry window minima of the requests (k_csr_finish's in sort mode)
+  int32_t csr_count;
+  int64_t P, nwin;
+  const int32_t *ptot;
+  const int64_t *ent_q;
+  int64_t *winmin;
   uint32_t key_off;        // W32 member loop: 64 * w_spread + 1 (plan_key_ok)
   uint64_t *pp;            // KP_PASS_PROFILE only
   const SolveStats *st;    // KP_PASS_PROFILE only (round index)
@@ -458,7 +591,25 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
 
 template <int D, int G, bool W32>
 __global__ __launch_bounds__(256) void k_plan(PlanArgs pa) {
-  if (KP_NREC && pa.pass == 0) {
+  if (pa.pass == 0 && pa.csr_count) {
+    // window w = this wave (the grid has >= ceil(A*K/64) waves): the smallest
+    // request per dim over its entries, a lower bound for k_accept's pruning
+    const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w < pa.nwin) {  // wave-uniform
+      const int64_t e = (int64_t)w * 64 + (threadIdx.x & 63);
+      const bool ok = e < *pa.ptot;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        uint64_t x = ok ? (uint64_t)pa.ent_q[(int64_t)d * pa.P + e] : ~0ull;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+          const uint64_t o = shfl_xor_u64(x, m);
+          x = o < x ? o : x;
+        }
+        if ((threadIdx.x & 63) == 0) pa.winmin[(int64_t)d * pa.nwin + w] = (int64_t)x;
+      }
+    }
+  } else if (KP_NREC && pa.pass == 0) {
     // the round's node records {node, seg_start, seg_end}: accept then finds
     // a node's bidder row with its first load (one thread per list entry; the
     // grid has >= A*K >= list-count threads)
@@ -837,6 +988,12 @@ static PlanArgs plan_args(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t p
   pa.arrive = c->d.arrive;
   pa.node_flag = c->d.node_flag;
   pa.key_off = (uint32_t)(64 * sp.w_spread + 1);
+  pa.csr_count = c->csr_mode;
+  pa.P = (int64_t)A * sp.n_cand;
+  pa.nwin = (pa.P + 63) / 64 + 64;
+  pa.ptot = c->d.counters + 33;
+  pa.ent_q = c->d.ent_q;
+  pa.winmin = c->d.winmin;
   pa.node_list = c->d.node_list;
   pa.nl_count = c->d.counters + 32;
   pa.seg_start = c->d.seg_start;
@@ -964,16 +1121,71 @@ size_t rocprim_temp_bytes(int32_t max_items) {
 }
 
 // node -> bidder inverse index of this round's candidates (one sort per round)
+
+static int ensure_bitmap(kp_ctx *c, int64_t words) {
+  const bool grow = !c->d.bm || words > c->cap_bm_words || c->N > c->cap_cnt_N;
+  if (grow) {
+    c->cap_bm_words = 0;
+    c->cap_cnt_N = 0;
+    for (void **p : {(void **)&c->d.bm, (void **)&c->d.rowinfo, (void **)&c->d.cnt})
+      if (*p) {
+        (void)hipFree(*p);
+        *p = nullptr;
+      }
+    const int64_t w = std::max<int64_t>(words, 64);
+    const int32_t nc = std::max(c->N, 64);
+    if (hipMalloc(reinterpret_cast<void **>(&c->d.bm), sizeof(uint32_t) * w) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&c->d.rowinfo), sizeof(uint2) * w) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&c->d.cnt), sizeof(int32_t) * nc) != hipSuccess)
+      return KP_ENOMEM;
+    c->cap_bm_words = w;
+    c->cap_cnt_N = nc;
+  }
+  // all-zero between rounds (k_csr_rows clears what k_csr_keys set); a
+  // round cut short between the two is repaired here
+  if (grow || c->bm_dirty)
+    KP_HIP(hipMemsetAsync(c->d.bm, 0, sizeof(uint32_t) * c->cap_bm_words, c->stream));
+  c->bm_dirty = false;
+  return KP_OK;
+}
+
 int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev) {
   const int64_t P = (int64_t)A * K;
   const int64_t nwin = (P + 63) / 64 + 64;
   const int64_t n = std::max<int64_t>(std::max<int64_t>(P, c->N), std::max<int64_t>(nwin, 64));
+  const int64_t Wb = ((int64_t)A + 31) / 32;
+  c->csr_mode = 0;
+  if (c->csr_count_enabled && P > 0 && c->N > 0 && (int64_t)c->N * Wb <= c->csr_bm_max) {
+    const int rc = ensure_bitmap(c, (int64_t)c->N * Wb);
+    if (rc == KP_OK)
+      c->csr_mode = 1;
+    else if (rc != KP_ENOMEM)  // out of memory: the radix sort needs none extra
+      return rc;
+  }
+  uint32_t *bm = c->csr_mode ? c->d.bm : nullptr;
+  if (bm) c->bm_dirty = true;
   hipLaunchKernelGGL(k_csr_keys, dim3(blocks(n, 256)), dim3(256), 0, c->stream, A, K, c->N, nwin,
                      c->d.cand, c->d.csr_kin, c->d.csr_vin, c->d.bid, c->d.win, c->d.seg_start,
                      c->d.pass_flag, c->d.node_flag, c->d.counters + 32, A_dev, c->d.stats,
-                     c->d.act, c->d.open, c->d.status);
+                     c->d.act, c->d.open, c->d.status, bm, Wb);
   KP_HIP(hipGetLastError());
   if (P == 0) return KP_OK;
+  if (c->csr_mode) {
+    hipLaunchKernelGGL(k_csr_rows, dim3((unsigned)((c->N + 15) / 16)), dim3(1024), 0, c->stream,
+                       c->N, Wb, c->d.bm, c->d.rowinfo, c->d.cnt);
+    KP_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_csr_scan, dim3(1), dim3(1024), 0, c->stream, c->N, c->d.cnt,
+                       c->d.seg_start, c->d.seg_end, c->d.node_list, c->d.nrec,
+                       c->d.counters + 32, c->d.counters + 33);
+    KP_HIP(hipGetLastError());
+    c->bm_dirty = false;
+    hipLaunchKernelGGL(k_csr_place, dim3(blocks(P, 256)), dim3(256), 0, c->stream, A, K, c->D,
+                       c->U, Wb, P, A_dev, c->d.cand, c->d.act, c->d.q, c->d.size, c->d.leader,
+                       c->d.seg_start, c->d.rowinfo, c->d.inv, c->d.ent_unit, c->d.ent_slot,
+                       c->d.ent_size, c->d.ent_lead, c->d.ent_q);
+    KP_HIP(hipGetLastError());
+    return KP_OK;
+  }
   unsigned bits = 1;
   while ((1ll << bits) <= c->N) ++bits;  // key N (invalid) must fit too
   size_t tb = c->d.temp_bytes;

@@ -230,6 +230,26 @@ def test_active_compaction_paths_parity(oracle, monkeypatch, cmax):
     _assert_same(g, o, f"KP_COMPACT_MAX={cmax}")
 
 
+@pytest.mark.parametrize("knobs", [
+    (("KP_CSR_SORT", "1"),),            # every round's bidder index by the radix sort
+    (("KP_CSR_BM_MAX", "40000"),),      # large early rounds sort, later rounds count
+])
+def test_csr_build_paths_parity(oracle, monkeypatch, knobs):
+    """The node -> bidder index is the same whether built by counting (slot
+    bitmap + row ranks, the default) or by the radix sort, also when a solve
+    switches between them from round to round."""
+    for k, v in knobs:
+        monkeypatch.setenv(k, v)
+    w = synth.config3(20_000, 2_000)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[3])
+    with Placer(device=0) as pl:
+        g = pl.place(w, p)
+        g2 = pl.place(w, p)  # the bitmap is all-zero again after a solve
+    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
+    _assert_same(g, o, f"csr {knobs}")
+    _assert_same(g2, o, f"csr {knobs} second solve")
+
+
 def few_class_workload(seed, J, N, D=4, classes=5, used_frac=0.5, affinity=True):
     """Nodes of a few capacity classes (with cap-0 dims inside a class) and
     random usage: the fused filter + score + top-K path's layout."""
