@@ -331,6 +331,8 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = std::getenv("KP_COMPACT_MAX")) c->compact_max = std::atoi(e);
   if (const char *e = std::getenv("KP_FUSED")) c->fused_enabled = std::atoi(e) != 0;
   if (const char *e = std::getenv("KP_ACC_LIST")) c->acc_list = std::atoi(e);
+  if (const char *e = std::getenv("KP_KEYS_MERGE")) c->keys_merge_enabled = std::atoi(e) != 0;
+  if (const char *e = std::getenv("KP_ROUND_BEGIN")) c->round_begin = std::atoi(e) != 0;
   if (const char *e = std::getenv("KP_CSR_SORT")) c->csr_count_enabled = std::atoi(e) == 0;
   if (const char *e = std::getenv("KP_CSR_BM_MAX")) c->csr_bm_max = std::atoll(e);
   if (const char *e = std::getenv("KP_ACC_WAVES")) c->acc_waves = std::max(0, std::atoi(e));
@@ -737,6 +739,12 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     // feasibility filter, so the bit mask (kp_score's second output) is not
     // materialised here
     if (fused) {
+      // one GPU, counting mode: the merge also does k_csr_keys' work
+      c->keys_in_merge = false;
+      if (c->world == 1 && c->keys_merge_enabled && r0 == 0 && rows > 0) {
+        KP_TRY(csr_prepare(c, rows, K));
+        c->keys_in_merge = c->csr_mode == 1;
+      }
       KP_TRY(launch_score_topk(c, sp, c->d.act_local + r0, rows, ksh, c->d.cand_local + r0 * K,
                                rows_dev));
     } else {

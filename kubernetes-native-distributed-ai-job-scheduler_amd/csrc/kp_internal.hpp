@@ -34,6 +34,20 @@ struct SolveStats {
   int64_t rounds, active_sum, passes, pad;
 };
 
+// The per-round work of k_csr_keys (kp_pass.hip) done by the fused
+// candidate merge (k_merge_tour) in counting mode on one GPU: open the slots,
+// set the slot bitmap bits, re-initialise the pass state (one launch fewer
+// per round). enabled = 0: k_csr_keys runs instead.
+struct RoundKeys {
+  int32_t enabled, A, K, N;
+  int64_t nwin, Wb, init_n;
+  uint32_t *bm, *bid;
+  int32_t *win, *seg_start, *pass_flag, *node_flag, *nl_count, *status;
+  uint8_t *open;
+  const int32_t *A_dev;
+  struct SolveStats *st;
+};
+
 // Scoring constants copied into kernel arguments (wave-uniform -> SGPRs).
 struct ScoreParams {
   int32_t D;
@@ -168,6 +182,10 @@ struct kp_ctx {
   int32_t acc_list = 1;  // KP_ACC_LIST=0: k_accept walks every node while entries >= nodes
   // KP_COMPACT_MAX: largest unit range compacted by the one-workgroup kernel
   int32_t compact_max = 262144;
+  bool round_begin = true;  // KP_ROUND_BEGIN=0: round start + compaction as two launches
+  // KP_KEYS_MERGE=0: k_csr_keys as its own launch; keys_in_merge: this
+  // round's merge did its work
+  bool keys_merge_enabled = true, keys_in_merge = false;
   // node -> bidder index by counting (KP_CSR_SORT=1: rocprim radix sort)
   bool csr_count_enabled = true, bm_dirty = false;
   int32_t csr_mode = 0;  // the current round's index: 1 counting, 0 sort
@@ -244,6 +262,10 @@ int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit,
 int launch_score_topk(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
                       int32_t ksh, int32_t *cand, const int32_t *rows_dev = nullptr);
 int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev = nullptr);
+// this round's index form (counting or sort) and its bitmap; called by
+// launch_csr_build, or before the candidate merge when that does k_csr_keys' work
+int csr_prepare(kp_ctx *c, int32_t A, int32_t K);
+RoundKeys round_keys_args(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev);
 int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass,
                 const int32_t *A_dev = nullptr);
 // direct (nullable): in, request the count stored by the compaction kernel

@@ -1149,10 +1149,8 @@ static int ensure_bitmap(kp_ctx *c, int64_t words) {
   return KP_OK;
 }
 
-int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev) {
+int csr_prepare(kp_ctx *c, int32_t A, int32_t K) {
   const int64_t P = (int64_t)A * K;
-  const int64_t nwin = (P + 63) / 64 + 64;
-  const int64_t n = std::max<int64_t>(std::max<int64_t>(P, c->N), std::max<int64_t>(nwin, 64));
   const int64_t Wb = ((int64_t)A + 31) / 32;
   c->csr_mode = 0;
   if (c->csr_count_enabled && P > 0 && c->N > 0 && (int64_t)c->N * Wb <= c->csr_bm_max) {
@@ -1162,13 +1160,50 @@ int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev) {
     else if (rc != KP_ENOMEM)  // out of memory: the radix sort needs none extra
       return rc;
   }
-  uint32_t *bm = c->csr_mode ? c->d.bm : nullptr;
-  if (bm) c->bm_dirty = true;
-  hipLaunchKernelGGL(k_csr_keys, dim3(blocks(n, 256)), dim3(256), 0, c->stream, A, K, c->N, nwin,
-                     c->d.cand, c->d.csr_kin, c->d.csr_vin, c->d.bid, c->d.win, c->d.seg_start,
-                     c->d.pass_flag, c->d.node_flag, c->d.counters + 32, A_dev, c->d.stats,
-                     c->d.act, c->d.open, c->d.status, bm, Wb);
-  KP_HIP(hipGetLastError());
+  if (c->csr_mode) c->bm_dirty = true;  // until k_csr_rows is enqueued
+  return KP_OK;
+}
+
+RoundKeys round_keys_args(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev) {
+  RoundKeys rk{};
+  const int64_t P = (int64_t)A * K;
+  rk.enabled = 1;
+  rk.A = A;
+  rk.K = K;
+  rk.N = c->N;
+  rk.nwin = (P + 63) / 64 + 64;
+  rk.Wb = ((int64_t)A + 31) / 32;
+  rk.init_n = std::max<int64_t>(std::max<int64_t>(c->N, rk.nwin), 64);
+  rk.bm = c->d.bm;
+  rk.bid = c->d.bid;
+  rk.win = c->d.win;
+  rk.seg_start = c->d.seg_start;
+  rk.pass_flag = c->d.pass_flag;
+  rk.node_flag = c->d.node_flag;
+  rk.nl_count = c->d.counters + 32;
+  rk.status = c->d.status;
+  rk.open = c->d.open;
+  rk.A_dev = A_dev;
+  rk.st = c->d.stats;
+  return rk;
+}
+
+int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev) {
+  const int64_t P = (int64_t)A * K;
+  const int64_t nwin = (P + 63) / 64 + 64;
+  const int64_t n = std::max<int64_t>(std::max<int64_t>(P, c->N), std::max<int64_t>(nwin, 64));
+  const int64_t Wb = ((int64_t)A + 31) / 32;
+  if (c->keys_in_merge) {  // the candidate merge did k_csr_keys' work (csr_prepare ran)
+    c->keys_in_merge = false;
+  } else {
+    KP_TRY(csr_prepare(c, A, K));
+    uint32_t *bm = c->csr_mode ? c->d.bm : nullptr;
+    hipLaunchKernelGGL(k_csr_keys, dim3(blocks(n, 256)), dim3(256), 0, c->stream, A, K, c->N, nwin,
+                       c->d.cand, c->d.csr_kin, c->d.csr_vin, c->d.bid, c->d.win, c->d.seg_start,
+                       c->d.pass_flag, c->d.node_flag, c->d.counters + 32, A_dev, c->d.stats,
+                       c->d.act, c->d.open, c->d.status, bm, Wb);
+    KP_HIP(hipGetLastError());
+  }
   if (P == 0) return KP_OK;
   if (c->csr_mode) {
     hipLaunchKernelGGL(k_csr_rows, dim3((unsigned)((c->N + 15) / 16)), dim3(1024), 0, c->stream,

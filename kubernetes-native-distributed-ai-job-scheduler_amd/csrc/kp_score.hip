@@ -932,18 +932,24 @@ __global__ void k_delta_check(int32_t K, int32_t N, int32_t D, const int32_t *__
 // lookback-state init + partition launches (2 kernels, ~13 us per round) for
 // the round's few-ten-thousand units.
 constexpr int kCompactBS = 1024, kCompactIPT = 16;
-__global__ __launch_bounds__(kCompactBS) void k_compact(const int32_t *__restrict__ flag, int32_t n,
-                                                        int32_t lo, int32_t *__restrict__ out,
-                                                        int32_t *__restrict__ count,
-                                                        int32_t *__restrict__ host_count) {
+// FROM_STATUS: the flags are status[lo + i] == kActive, read straight from the
+// unit status (k_round_begin); else the flag array of k_round_start
+template <bool FROM_STATUS>
+__device__ __forceinline__ void compact_wg(const int32_t *__restrict__ flag, int32_t n,
+                                           int32_t lo, int32_t *__restrict__ out,
+                                           int32_t *__restrict__ count,
+                                           int32_t *__restrict__ host_count) {
   __shared__ int32_t wsum[kCompactBS / kWave];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  // 16-B loads need a 16-B aligned start (status + lo: lo % 4 == 0)
+  const bool vec = !FROM_STATUS || (lo & 3) == 0;
+  const int32_t *src = FROM_STATUS ? flag + lo : flag;
   int32_t carry = 0;
   for (int32_t base = 0; base < n; base += kCompactBS * kCompactIPT) {
     const int32_t i0 = base + t * kCompactIPT;
     int32_t f[kCompactIPT];
-    if (i0 + kCompactIPT <= n) {  // flag is 16-B aligned (device allocation), i0 % 16 == 0
-      const int4 *p = reinterpret_cast<const int4 *>(flag + i0);
+    if (vec && i0 + kCompactIPT <= n) {  // 16-B aligned (device allocation), i0 % 16 == 0
+      const int4 *p = reinterpret_cast<const int4 *>(src + i0);
 #pragma unroll
       for (int v = 0; v < kCompactIPT / 4; ++v) {
         const int4 x = p[v];
@@ -951,7 +957,12 @@ __global__ __launch_bounds__(kCompactBS) void k_compact(const int32_t *__restric
       }
     } else {
 #pragma unroll
-      for (int k = 0; k < kCompactIPT; ++k) f[k] = i0 + k < n ? flag[i0 + k] : 0;
+      for (int k = 0; k < kCompactIPT; ++k)
+        f[k] = i0 + k < n ? src[i0 + k] : (FROM_STATUS ? -1 : 0);
+    }
+    if (FROM_STATUS) {
+#pragma unroll
+      for (int k = 0; k < kCompactIPT; ++k) f[k] = f[k] == kActive ? 1 : 0;
     }
     int32_t c = 0;
 #pragma unroll
@@ -985,6 +996,50 @@ __global__ __launch_bounds__(kCompactBS) void k_compact(const int32_t *__restric
     if (host_count) __hip_atomic_store(host_count, carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
+
+__global__ __launch_bounds__(kCompactBS) void k_compact(const int32_t *__restrict__ flag, int32_t n,
+                                                        int32_t lo, int32_t *__restrict__ out,
+                                                        int32_t *__restrict__ count,
+                                                        int32_t *__restrict__ host_count) {
+  compact_wg<false>(flag, n, lo, out, count, host_count);
+}
+
+// Round start and compaction in ONE launch (one-workgroup compaction range):
+// workgroup 0 compacts the active units of [lo, lo + n) straight from the
+// unit status, workgroups 1.. pack the round's 32-bit node planes (the work
+// of k_round_start + k_compact, one launch fewer per round).
+template <int D>
+__global__ __launch_bounds__(kCompactBS) void k_round_begin(
+    const int32_t *__restrict__ status, int32_t lo, int32_t n, int32_t *__restrict__ out,
+    int32_t *__restrict__ count, int32_t *__restrict__ host_count,
+    const int64_t *__restrict__ cap, const int64_t *__restrict__ used,
+    const uint32_t *__restrict__ R32, const uint32_t *__restrict__ K32,
+    const int64_t *__restrict__ base, const int32_t *__restrict__ topo,
+    const int32_t *__restrict__ perm, const int32_t *__restrict__ colnode, int32_t N, int32_t P,
+    int32_t full, ScoreParams sp, uint32_t *__restrict__ np) {
+  if (blockIdx.x == 0) {
+    compact_wg<true>(status, n, lo, out, count, host_count);
+    return;
+  }
+  const int i = (blockIdx.x - 1) * kCompactBS + threadIdx.x;
+  if (i < P) pack_node<D>(cap, used, R32, K32, base, topo, perm, colnode, N, P, full != 0, sp, np, i);
+}
+
+template <int D>
+struct RoundBeginL {
+  static int run(kp_ctx *c, int32_t lo, int32_t n, int32_t *host_count) {
+    const int32_t P = !c->fits32 || c->N == 0 ? 0 : c->pack_fused ? c->fz_P : (c->N + 1023) & ~1023;
+    hipLaunchKernelGGL((k_round_begin<D>), dim3(1 + blocks(P, kCompactBS)), dim3(kCompactBS), 0,
+                       c->stream, c->d.status, lo, n, c->d.act_local, c->d.counters, host_count,
+                       c->d.cap, c->d.used, c->d.R32, c->d.K32, c->d.base, c->d.topo,
+                       c->pack_canonical ? c->d.perm : nullptr,
+                       c->pack_fused ? c->d.colnode : nullptr, c->N, P, c->pack_full ? 1 : 0,
+                       c->pack_sp, c->d.np32);
+    KP_HIP(hipGetLastError());
+    if (P > 0) c->pack_full = false;  // capacity planes in place for this layout
+    return KP_OK;
+  }
+};
 
 template <int D>
 struct ScoreL {
@@ -1210,6 +1265,16 @@ int launch_delta(kp_ctx *c, int32_t K, int32_t *bad_host) {
 int launch_active_async(kp_ctx *c, int32_t lo, int32_t hi, int32_t *count_host, bool *direct) {
   const int32_t n = hi - lo;
   if (n <= 0) return KP_EINVAL;
+  if (n <= c->compact_max && c->round_begin) {  // one launch: compaction + node planes
+    const bool dir = direct && c->count_direct && c->pinned_coh;
+    if (direct) *direct = dir;
+    if (dir) __atomic_store_n(c->pinned_coh, -1, __ATOMIC_RELAXED);  // the sentinel the host waits on
+    KP_TRY(dispatch_D<RoundBeginL>(c->D, c, lo, n, dir ? c->pinned_coh : nullptr));
+    if (!dir)
+      KP_HIP(hipMemcpyAsync(count_host, c->d.counters, sizeof(int32_t), hipMemcpyDeviceToHost,
+                            c->stream));
+    return KP_OK;
+  }
   KP_TRY(launch_round_start(c, lo, hi, c->d.flag));
   size_t tb = c->d.temp_bytes;
   // the one-workgroup compaction stores the count into coherent pinned

@@ -520,6 +520,30 @@ void k_score_topk(
 // max of the heads, and only the owner of the max advances its list (one LDS
 // read). K x (one wave max + one LDS read) per row instead of K passes over
 // all ntiles*K keys. Dynamic LDS: 4 rows x ntiles*K keys.
+// k_csr_keys' per-round state reset, thread t of the merge's extra workgroups
+// (rk.enabled): round statistics, the previous round's productive passes,
+// node segments / flags, window flags
+__device__ __forceinline__ void round_keys_init(const RoundKeys &rk, int64_t t) {
+  if (t == 0) {
+    const int32_t Aa = rk.A_dev ? min(rk.A, *rk.A_dev) : rk.A;
+    if (Aa > 0) {
+      rk.st->rounds += 1;
+      rk.st->active_sum += Aa;
+    }
+    *rk.nl_count = 0;
+  }
+  if (t < rk.N) {
+    rk.seg_start[t] = -1;
+    rk.node_flag[t] = -1;
+  }
+  if (t < rk.nwin) rk.win[t] = -1;
+  if (t < 64) {
+    if (rk.pass_flag[t] != 0)
+      atomicAdd(reinterpret_cast<unsigned long long *>(&rk.st->passes), 1ull);
+    rk.pass_flag[t] = 0;
+  }
+}
+
 template <int LPL>
 __global__ __launch_bounds__(256) void k_merge_tour(ScoreParams sp, const uint64_t *__restrict__ part,
                                                     int32_t ntiles,
@@ -527,9 +551,14 @@ __global__ __launch_bounds__(256) void k_merge_tour(ScoreParams sp, const uint64
                                                     const uint32_t *__restrict__ salt, int32_t rows,
                                                     const int32_t *__restrict__ rows_dev,
                                                     const int32_t *__restrict__ perm,
-                                                    int32_t *__restrict__ cand) {
+                                                    int32_t *__restrict__ cand, RoundKeys rk) {
   extern __shared__ uint64_t slist[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int rblocks = (rows + 3) / 4;
+  if ((int)blockIdx.x >= rblocks) {  // rk.enabled: the extra workgroups
+    round_keys_init(rk, (int64_t)(blockIdx.x - rblocks) * 256 + threadIdx.x);
+    return;
+  }
   const int row = blockIdx.x * 4 + wave;
   if (row >= rows || (rows_dev && row >= *rows_dev)) return;  // wave-uniform, no barrier below
   const int K = sp.n_cand, M = ntiles * K;
@@ -550,6 +579,7 @@ __global__ __launch_bounds__(256) void k_merge_tour(ScoreParams sp, const uint64
   const uint32_t sl = sp.tie_rotated ? salt[rows_unit[row]] : 0u;
   const uint32_t inv = sp.tie_rotated ? kTieMulInv : 1u;
   int32_t *out = cand + (int64_t)row * K;
+  int32_t mine = -1;  // rk.enabled: lane it keeps candidate it
   for (int it = 0; it < K; ++it) {
     uint64_t b = v[0];
 #pragma unroll
@@ -568,9 +598,25 @@ __global__ __launch_bounds__(256) void k_merge_tour(ScoreParams sp, const uint64
         ++h[j];
         v[j] = h[j] < K ? L[t * K + h[j]] : 0ull;
       }
-    if (lane == 0) {  // canonical position -> node (a position is always < N)
+    if (rk.enabled) {  // every lane maps the position (one broadcast load)
+      const int32_t pos = key_node(m, sl, inv);
+      const int32_t nd = (uint32_t)pos < (uint32_t)sp.N ? perm[pos] : -1;
+      if (lane == 0) out[it] = nd;
+      if (lane == it) mine = nd;
+    } else if (lane == 0) {  // canonical position -> node (a position is always < N)
       const int32_t pos = key_node(m, sl, inv);
       out[it] = (uint32_t)pos < (uint32_t)sp.N ? perm[pos] : -1;
+    }
+  }
+  if (rk.enabled) {  // k_csr_keys' work for slot `row` (single GPU: slot = row)
+    if (lane < K) {
+      rk.bid[(int64_t)row * K + lane] = 0xFFFFFFFFu;  // kNoBid
+      if (mine >= 0) atomicOr(&rk.bm[(int64_t)mine * rk.Wb + (row >> 5)], 1u << (row & 31));
+    }
+    const int32_t first = __shfl(mine, 0, 64);
+    if (lane == 0) {
+      rk.open[row] = first >= 0 ? 1 : 0;
+      if (first < 0) rk.status[rows_unit[row]] = kNoFit;
     }
   }
 }
@@ -598,11 +644,13 @@ struct TopkL {
 #undef KP_FZ
     KP_HIP(hipGetLastError());
     const int M = ntiles * sp.n_cand;
-    const dim3 mg(blocks(rows, 4));
+    RoundKeys rk{};
+    if (c->keys_in_merge) rk = round_keys_args(c, rows, sp.n_cand, rows_dev);
+    const dim3 mg(blocks(rows, 4) + (rk.enabled ? blocks(rk.init_n, 256) : 0));
     const size_t lds = (size_t)4 * M * sizeof(uint64_t);  // <= 64 KB (M <= 2,048)
 #define KP_MG(LPL)                                                                       \
   hipLaunchKernelGGL((k_merge_tour<LPL>), mg, dim3(256), lds, c->stream, sp, c->d.part, \
-                     ntiles, rows_unit, c->d.salt, rows, rows_dev, c->d.perm, cand)
+                     ntiles, rows_unit, c->d.salt, rows, rows_dev, c->d.perm, cand, rk)
     if (ntiles <= 64)
       KP_MG(1);
     else if (ntiles <= 128)
