@@ -225,8 +225,10 @@ __global__ void k_csr_finish(int32_t P, int32_t N, int32_t K, int32_t D, int32_t
 // scans the row lengths into node segments (node order). k_csr_place then
 // gives candidate (a, c) its entry e = segment start + rank of bit a, so each
 // node's bidder row is in slot (= rank) order: a stable counting sort keyed by
-// node id. (A last-workgroup-done scan inside k_csr_rows needs a device-scope
-// fence per wave: 150-280 us per launch measured, vs one more launch.)
+// node id. (Measured alternatives to the separate scan launch, ~12 us per
+// round for rows + scan: a last-workgroup-done scan inside k_csr_rows needs a
+// device-scope fence per wave, 150-280 us per launch; a decoupled look-back
+// over the 16-row blocks, 16 us per launch.)
 __global__ __launch_bounds__(1024) void k_csr_rows(int32_t N, int64_t Wb,
                                                    uint32_t *__restrict__ bm,
                                                    uint2 *__restrict__ rowinfo,
