@@ -745,14 +745,18 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
         KP_TRY(csr_prepare(c, rows, K));
         c->keys_in_merge = c->csr_mode == 1;
       }
-      KP_TRY(launch_score_topk(c, sp, c->d.act_local + r0, rows, ksh, c->d.cand_local + r0 * K,
-                               rows_dev));
+      // the profiling bracket ends right after k_score_topk (before the merge)
+      c->fz_end_event = c->profiling ? ke.b : nullptr;
+      const int rc = launch_score_topk(c, sp, c->d.act_local + r0, rows, ksh,
+                                       c->d.cand_local + r0 * K, rows_dev);
+      c->fz_end_event = nullptr;
+      KP_TRY(rc);
     } else {
       KP_TRY(launch_score(c, sp, c->d.act_local + r0, rows, c->d.score, nullptr, c->d.q, U,
                           rows_dev));
     }
     if (c->profiling) {
-      KP_HIP(hipEventRecord(ke.b, c->stream));
+      if (!fused) KP_HIP(hipEventRecord(ke.b, c->stream));
       kev.push_back(ke);
     }
     if (!fused)

@@ -165,6 +165,7 @@ struct kp_ctx {
   int64_t max_pairs_matrix = 0;
   hipStream_t stream = nullptr;
   bool profiling = false;
+  hipEvent_t fz_end_event = nullptr;  // profiling: recorded right after k_score_topk
   // test knobs, read from the environment at kp_create (never set in
   // production): KP_SELECT_LDS_CAP shrinks the threshold select's survivor
   // buffer (forces its threshold-raise path), KP_SELECT_GENERIC=1 forces the

@@ -643,6 +643,7 @@ struct TopkL {
     }
 #undef KP_FZ
     KP_HIP(hipGetLastError());
+    if (c->fz_end_event) KP_HIP(hipEventRecord(c->fz_end_event, c->stream));
     const int M = ntiles * sp.n_cand;
     RoundKeys rk{};
     if (c->keys_in_merge) rk = round_keys_args(c, rows, sp.n_cand, rows_dev);
