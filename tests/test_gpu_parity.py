@@ -251,6 +251,17 @@ def test_csr_build_paths_parity(oracle, monkeypatch, knobs):
     _assert_same(g2, o, f"csr {knobs} second solve")
 
 
+def test_csr_scan_many_nodes(oracle):
+    """More than one 65,536-node tile in the node scan of the counting-mode
+    bidder index (running carry between tiles)."""
+    w = synth.config3(3_000, 70_000)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[3])
+    with Placer(device=0) as pl:
+        g = pl.place(w, p)
+    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
+    _assert_same(g, o, "csr scan 70k nodes")
+
+
 def few_class_workload(seed, J, N, D=4, classes=5, used_frac=0.5, affinity=True):
     """Nodes of a few capacity classes (with cap-0 dims inside a class) and
     random usage: the fused filter + score + top-K path's layout."""
