@@ -179,7 +179,9 @@ struct kp_ctx {
   int32_t fz_wg_target = 2048;  // KP_FZ_WG_TARGET: target workgroups of k_score_topk
   bool fz_h16 = true;     // KP_FZ_H16=0: 32-bit LDS scores in k_score_topk
   int32_t fz_tie_bits = 0;  // KP_FZ_TIE_BITS=b (tests): b select-phase tie bits, forces collisions
-  int32_t acc_waves = 0;  // KP_ACC_WAVES: largest k_accept grid in waves (0 = one per node)
+  // KP_ACC_WAVES: largest k_accept grid in waves, grid-stride over the rest (0 =
+  // one per node); 2,048: config #5 batches -2 %, config #3 neutral (tools/ab_*env.sh)
+  int32_t acc_waves = 2048;
   int32_t acc_list = 1;  // KP_ACC_LIST=0: k_accept walks every node while entries >= nodes
   // KP_COMPACT_MAX: largest unit range compacted by the one-workgroup kernel
   int32_t compact_max = 262144;

@@ -234,6 +234,9 @@ def test_active_compaction_paths_parity(oracle, monkeypatch, cmax):
     (("KP_CSR_SORT", "1"),),            # every round's bidder index by the radix sort
     (("KP_CSR_BM_MAX", "40000"),),      # large early rounds sort, later rounds count
     (("KP_KEYS_MERGE", "0"), ("KP_ROUND_BEGIN", "0")),  # k_csr_keys, k_round_start + k_compact launches
+    (("KP_ACC_WAVES", "0"),),           # one accept wave per listed node
+    (("KP_ACC_WAVES", "64"),),          # accept grid-stride over many nodes per wave
+    (("KP_ACC_LIST", "0"),),            # accept walks every node once entries >= nodes
 ])
 def test_csr_build_paths_parity(oracle, monkeypatch, knobs):
     """The node -> bidder index is the same whether built by counting (slot
