@@ -579,7 +579,10 @@ __global__ __launch_bounds__(256) void k_merge_tour(ScoreParams sp, const uint64
   const uint32_t sl = sp.tie_rotated ? salt[rows_unit[row]] : 0u;
   const uint32_t inv = sp.tie_rotated ? kTieMulInv : 1u;
   int32_t *out = cand + (int64_t)row * K;
-  int32_t mine = -1;  // rk.enabled: lane it keeps candidate it
+  // lane it keeps the canonical position of candidate it; the positions are
+  // mapped to nodes after the loop with ONE load per lane (a perm load + store
+  // inside the loop serialises K memory latencies)
+  int32_t mypos = -1;
   for (int it = 0; it < K; ++it) {
     uint64_t b = v[0];
 #pragma unroll
@@ -587,10 +590,7 @@ __global__ __launch_bounds__(256) void k_merge_tour(ScoreParams sp, const uint64
     const uint32_t mhi = wave_max32((uint32_t)(b >> 32));
     const uint32_t mlo = wave_max32((uint32_t)(b >> 32) == mhi ? (uint32_t)b : 0u);
     const uint64_t m = ((uint64_t)mhi << 32) | mlo;
-    if (m == 0) {  // fewer than K feasible nodes
-      if (lane >= it && lane < K) out[lane] = -1;
-      break;
-    }
+    if (m == 0) break;  // fewer than K feasible nodes: lanes >= it keep -1
 #pragma unroll
     for (int j = 0; j < LPL; ++j)
       if (v[j] == m) {  // keys are unique: one list of one lane
@@ -598,16 +598,11 @@ __global__ __launch_bounds__(256) void k_merge_tour(ScoreParams sp, const uint64
         ++h[j];
         v[j] = h[j] < K ? L[t * K + h[j]] : 0ull;
       }
-    if (rk.enabled) {  // every lane maps the position (one broadcast load)
-      const int32_t pos = key_node(m, sl, inv);
-      const int32_t nd = (uint32_t)pos < (uint32_t)sp.N ? perm[pos] : -1;
-      if (lane == 0) out[it] = nd;
-      if (lane == it) mine = nd;
-    } else if (lane == 0) {  // canonical position -> node (a position is always < N)
-      const int32_t pos = key_node(m, sl, inv);
-      out[it] = (uint32_t)pos < (uint32_t)sp.N ? perm[pos] : -1;
-    }
+    if (lane == it) mypos = key_node(m, sl, inv);
   }
+  // canonical position -> node (a position is always < N)
+  const int32_t mine = (uint32_t)mypos < (uint32_t)sp.N ? perm[mypos] : -1;
+  if (lane < K) out[lane] = mine;
   if (rk.enabled) {  // k_csr_keys' work for slot `row` (single GPU: slot = row)
     if (lane < K) {
       rk.bid[(int64_t)row * K + lane] = 0xFFFFFFFFu;  // kNoBid
