@@ -68,14 +68,6 @@ static int fail(int code, const char *fmt, ...) {
   return code;
 }
 
-static uint32_t fmix32(uint32_t h) {
-  h ^= h >> 16;
-  h *= 0x85EBCA6Bu;
-  h ^= h >> 13;
-  h *= 0xC2B2AE35u;
-  h ^= h >> 16;
-  return h;
-}
 
 // ---- validation, identical to oracle/kp_oracle.c check_params/check_nodes ----
 static int check_params(const kp_params *p, int32_t D) {
@@ -543,19 +535,46 @@ static int load_jobs_impl(kp_ctx *c, int32_t J, const int64_t *req, const int32_
       j = e;
     }
     if (gang_id) {  // a gang id may not reappear in a later run
-      std::vector<int32_t> ids;
-      for (size_t u = 0; u < leader.size(); ++u)
-        if (gang_id[leader[u]] >= 0) ids.push_back(gang_id[leader[u]]);
-      std::sort(ids.begin(), ids.end());
-      auto it = std::adjacent_find(ids.begin(), ids.end());
-      if (it != ids.end()) return fail(KP_EINVAL, "kp_load_jobs: gang id %d reappears", *it);
+      int32_t idmax = -1;
+      for (size_t u = 0; u < leader.size(); ++u) idmax = std::max(idmax, gang_id[leader[u]]);
+      if (idmax >= 0 && (int64_t)idmax < 8 * (int64_t)leader.size() + 4096) {
+        std::vector<uint8_t> seen((size_t)idmax + 1, 0);  // ids are usually CR indices
+        for (size_t u = 0; u < leader.size(); ++u) {
+          const int32_t g = gang_id[leader[u]];
+          if (g < 0) continue;
+          if (seen[(size_t)g]) return fail(KP_EINVAL, "kp_load_jobs: gang id %d reappears", g);
+          seen[(size_t)g] = 1;
+        }
+      } else if (idmax >= 0) {
+        std::vector<int32_t> ids;
+        for (size_t u = 0; u < leader.size(); ++u)
+          if (gang_id[leader[u]] >= 0) ids.push_back(gang_id[leader[u]]);
+        std::sort(ids.begin(), ids.end());
+        auto it = std::adjacent_find(ids.begin(), ids.end());
+        if (it != ids.end()) return fail(KP_EINVAL, "kp_load_jobs: gang id %d reappears", *it);
+      }
     }
     const int32_t U = (int32_t)leader.size();
     std::vector<int32_t> ord(U);
-    for (int32_t u = 0; u < U; ++u) ord[u] = u;
-    // leaders ascend with u, so a stable sort on priority gives (prio desc, leader asc)
-    std::stable_sort(ord.begin(), ord.end(),
-                     [&](int32_t a, int32_t b) { return uprio[a] > uprio[b]; });
+    // rank order (prio desc, leader asc): leaders ascend with u, so a stable
+    // order by priority; a counting sort when the priorities span a small
+    // range (priority tiers), else a stable comparison sort
+    int32_t pmin = INT32_MAX, pmax = INT32_MIN;
+    for (int32_t u = 0; u < U; ++u) {
+      pmin = std::min(pmin, uprio[u]);
+      pmax = std::max(pmax, uprio[u]);
+    }
+    if (U > 0 && (int64_t)pmax - pmin < 65536) {
+      const int32_t R = pmax - pmin + 1;
+      std::vector<int32_t> at((size_t)R + 1, 0);
+      for (int32_t u = 0; u < U; ++u) ++at[(size_t)(pmax - uprio[u]) + 1];
+      for (int32_t r = 0; r < R; ++r) at[(size_t)r + 1] += at[(size_t)r];
+      for (int32_t u = 0; u < U; ++u) ord[(size_t)at[(size_t)(pmax - uprio[u])]++] = u;
+    } else {
+      for (int32_t u = 0; u < U; ++u) ord[u] = u;
+      std::stable_sort(ord.begin(), ord.end(),
+                       [&](int32_t a, int32_t b) { return uprio[a] > uprio[b]; });
+    }
     c->h_leader.resize(U);
     c->h_size.resize(U);
     c->h_prio.resize(U);
@@ -577,15 +596,33 @@ static int load_jobs_impl(kp_ctx *c, int32_t J, const int64_t *req, const int32_
   KP_TRY(ensure_units(c, U, J));
   KP_TRY(ensure_q(c, U, D));
   if (U > 0) {
-    KP_HIP(hipMemcpyAsync(c->d.leader, c->h_leader.data(), sizeof(int32_t) * U,
+    // one pinned staging block (DMA straight from it; pageable copies go
+    // through the runtime's staging buffers one call at a time)
+    const size_t need = sizeof(int64_t) * D * U + 4 * sizeof(int32_t) * U;
+    if (need > c->stage_bytes) {
+      if (c->stage) (void)hipHostFree(c->stage);
+      c->stage = nullptr;
+      c->stage_bytes = 0;
+      if (hipHostMalloc(&c->stage, need, hipHostMallocDefault) != hipSuccess) {
+        c->stage = nullptr;
+        return fail(KP_ENOMEM, "kp_load_jobs: pinned staging of %zu bytes", need);
+      }
+      c->stage_bytes = need;
+    }
+    int64_t *sq = static_cast<int64_t *>(c->stage);
+    int32_t *s32 = reinterpret_cast<int32_t *>(sq + (size_t)D * U);
+    std::memcpy(sq, c->h_q.data(), sizeof(int64_t) * D * U);
+    std::memcpy(s32, c->h_leader.data(), sizeof(int32_t) * U);
+    std::memcpy(s32 + U, c->h_size.data(), sizeof(int32_t) * U);
+    std::memcpy(s32 + 2 * (size_t)U, c->h_prio.data(), sizeof(int32_t) * U);
+    std::memcpy(s32 + 3 * (size_t)U, c->h_aff.data(), sizeof(int32_t) * U);
+    KP_HIP(hipMemcpyAsync(c->d.q, sq, sizeof(int64_t) * D * U, hipMemcpyHostToDevice, c->stream));
+    KP_HIP(hipMemcpyAsync(c->d.leader, s32, sizeof(int32_t) * U, hipMemcpyHostToDevice, c->stream));
+    KP_HIP(hipMemcpyAsync(c->d.size, s32 + U, sizeof(int32_t) * U, hipMemcpyHostToDevice,
+                          c->stream));
+    KP_HIP(hipMemcpyAsync(c->d.uprio, s32 + 2 * (size_t)U, sizeof(int32_t) * U,
                           hipMemcpyHostToDevice, c->stream));
-    KP_HIP(hipMemcpyAsync(c->d.size, c->h_size.data(), sizeof(int32_t) * U,
-                          hipMemcpyHostToDevice, c->stream));
-    KP_HIP(hipMemcpyAsync(c->d.q, c->h_q.data(), sizeof(int64_t) * D * U,
-                          hipMemcpyHostToDevice, c->stream));
-    KP_HIP(hipMemcpyAsync(c->d.uprio, c->h_prio.data(), sizeof(int32_t) * U,
-                          hipMemcpyHostToDevice, c->stream));
-    KP_HIP(hipMemcpyAsync(c->d.aff, c->h_aff.data(), sizeof(int32_t) * U,
+    KP_HIP(hipMemcpyAsync(c->d.aff, s32 + 3 * (size_t)U, sizeof(int32_t) * U,
                           hipMemcpyHostToDevice, c->stream));
   }
   KP_HIP(hipStreamSynchronize(c->stream));
@@ -653,15 +690,6 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   const int64_t Ns = (N + 63) & ~63;
   KP_TRY(prep_for(c, p));
   KP_TRY(launch_node_rec(c));
-  // salts of the rotated tie-break
-  {
-    std::vector<uint32_t> salt(U);
-    for (int32_t u = 0; u < U; ++u) salt[u] = fmix32((uint32_t)c->h_leader[u] ^ p->tie_seed);
-    if (U > 0)
-      KP_HIP(hipMemcpyAsync(c->d.salt, salt.data(), sizeof(uint32_t) * U, hipMemcpyHostToDevice,
-                            c->stream));
-    KP_HIP(hipStreamSynchronize(c->stream));
-  }
   {  // every buffer the solve's kernels touch exists (never launch on a null)
     const DevState &d = c->d;
     const void *need[] = {d.cap, d.used, d.R32, d.K32, d.base, d.topo, d.perm, d.np32, d.q, d.leader,
@@ -674,7 +702,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     for (const void *ptr : need)
       if (!ptr) return fail(KP_ENOMEM, "kp_solve: a device buffer is missing");
   }
-  KP_TRY(launch_reset_units(c));
+  KP_TRY(launch_reset_units(c, p->tie_seed));  // also the salts of the rotated tie-break
   c->pack_sp = sp;
   c->pack_canonical = true;  // the solve scores in canonical column order
   const int32_t shard = c->u_hi - c->u_lo;
@@ -1112,6 +1140,7 @@ void kp_destroy(kp_ctx *c) {
   }
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->pinned_coh) (void)hipHostFree(c->pinned_coh);
+  if (c->stage) (void)hipHostFree(c->stage);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }

@@ -228,6 +228,8 @@ struct kp_ctx {
   // coherent pinned word the compaction kernel stores the round's active
   // count into (KP_COUNT_DIRECT=0: copy it with hipMemcpyAsync instead)
   int32_t *pinned_coh = nullptr;
+  void *stage = nullptr;  // pinned staging of kp_load_jobs' unit arrays
+  size_t stage_bytes = 0;
   bool count_direct = true;
   bool host_prof = false;  // KP_HOST_PROF=1: host enqueue / wait split per solve on stderr
   kp::DevState d;
@@ -280,7 +282,8 @@ int launch_accept(kp_ctx *c, const ScoreParams &sp, int32_t pass, int32_t A);
 int launch_node_rec(kp_ctx *c);
 void launch_probe(kp_ctx *c, const ScoreParams &sp, int32_t A);
 int launch_active(kp_ctx *c, int32_t lo, int32_t hi, int32_t *A_host);
-int launch_reset_units(kp_ctx *c);
+// unit status, job outputs and the per-unit tie-break salts of a solve
+int launch_reset_units(kp_ctx *c, uint32_t tie_seed);
 int launch_finalize(kp_ctx *c);
 // multi-GPU exchange blocks: [count, (unit, K candidates) x B] per rank; pack
 // reads the device count counters[0], unpack writes the global count to

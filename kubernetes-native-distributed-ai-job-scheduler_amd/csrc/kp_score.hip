@@ -827,11 +827,25 @@ __global__ __launch_bounds__(256) void k_select(ScoreParams sp,
 // ---------------------------------------------------------------------------
 // round bookkeeping
 // ---------------------------------------------------------------------------
+// per-unit salt of the rotated tie-break: fmix32(leader ^ seed)
+__device__ __forceinline__ uint32_t fmix32_dev(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+
 __global__ void k_reset_units(int32_t *__restrict__ status, int32_t U,
                               int32_t *__restrict__ job_node, int32_t *__restrict__ job_score,
-                              int32_t J) {
+                              int32_t J, const int32_t *__restrict__ leader,
+                              uint32_t *__restrict__ salt, uint32_t seed) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < U) status[i] = kActive;
+  if (i < U) {
+    status[i] = kActive;
+    salt[i] = fmix32_dev((uint32_t)leader[i] ^ seed);
+  }
   if (i < J) {
     job_node[i] = -1;
     job_score[i] = KP_SCORE_NONE;
@@ -1292,11 +1306,11 @@ int launch_active_async(kp_ctx *c, int32_t lo, int32_t hi, int32_t *count_host, 
   return KP_OK;
 }
 
-int launch_reset_units(kp_ctx *c) {
+int launch_reset_units(kp_ctx *c, uint32_t tie_seed) {
   const int32_t n = c->U > c->J ? c->U : c->J;
   if (n <= 0) return KP_OK;
   hipLaunchKernelGGL(k_reset_units, dim3(blocks(n, 256)), dim3(256), 0, c->stream, c->d.status,
-                     c->U, c->d.job_node, c->d.job_score, c->J);
+                     c->U, c->d.job_node, c->d.job_score, c->J, c->d.leader, c->d.salt, tie_seed);
   KP_HIP(hipGetLastError());
   return KP_OK;
 }

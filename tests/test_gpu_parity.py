@@ -165,6 +165,21 @@ def test_place_random_parity(oracle, placer, seed):
     _assert_same(g, o, f"seed {seed}")
 
 
+@pytest.mark.parametrize("spread", [3, 1 << 30])
+def test_place_priority_range_parity(oracle, placer, spread):
+    """Unit rank order (prio desc, leader asc) by the host's counting sort
+    (priorities within a small range) and by its comparison-sort fallback."""
+    w = random_workload(77, J=1200, N=150)
+    rng = np.random.default_rng(5)
+    cr = np.cumsum(np.r_[1, (w.gang_id[1:] != w.gang_id[:-1]) | (w.gang_id[1:] < 0)]) - 1
+    pcr = rng.integers(-spread, spread + 1, size=int(cr.max()) + 1).astype(np.int32)
+    w = synth.Workload(w.J, w.N, w.D, w.req, w.cap, w.used, pcr[cr], w.gang_id, w.gang_size,
+                       w.topo, name=f"prio{spread}")
+    p = _abi.default_params()
+    g, o = _place_both(oracle, placer, w, p)
+    _assert_same(g, o, f"priority spread {spread}")
+
+
 def test_place_config2_parity(oracle, placer):
     w = synth.config2(10_000, 1_000)
     p = _abi.default_params(**synth.CONFIG_PARAMS[2])
@@ -492,6 +507,13 @@ def test_invalid_inputs_rejected(placer):
     req = np.array([[1, 2]] * 4, np.int64)
     with pytest.raises(KPlaceError):
         placer.load_jobs(req, gang_id=np.array([7, 7], np.int32))
+    # a gang id reappearing in a later run: small ids (seen-table check) and
+    # ids far above the unit count (sorted check)
+    req3 = np.ones((4, 3), np.int64)
+    for gid in (5, 2_000_000_000):
+        with pytest.raises(KPlaceError) as e:
+            placer.load_jobs(req3, gang_id=np.array([gid, -1, gid], np.int32))
+        assert e.value.code == _abi.KP_EINVAL
     placer.load_jobs(np.ones((4, 2), np.int64))
     bad = _abi.default_params(n_cand=0)
     with pytest.raises(KPlaceError):
