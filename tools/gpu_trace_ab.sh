@@ -10,7 +10,7 @@ for setting in "$@"; do
   export $setting
   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-stream --no-config4 --place-steps 0 --no-kernel-events > $OUT/bench.log 2>&1 || exit $?
   echo "== $setting"
-  python3 tools/ktrace_sum.py $OUT/run_kernel_trace.csv k_merge_tour,k_csr_scan,k_round_begin || exit 1
+  python3 tools/ktrace_sum.py $OUT/run_kernel_trace.csv k_accept,k_plan || exit 1
   rm -f $OUT/run_kernel_trace.csv
   i=$((i+1))
 done

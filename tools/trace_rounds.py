@@ -10,7 +10,7 @@ which = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2] != "--all" else -1
 end = starts[which + 1] if which != -1 and which + 1 < len(starts) else len(rows)
 seq = rows[starts[which]:end]
 dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-rs = [i for i, r in enumerate(seq) if "k_round_start" in r["Kernel_Name"]]
+rs = [i for i, r in enumerate(seq) if ("k_round_start" in r["Kernel_Name"] or "k_round_begin" in r["Kernel_Name"])]
 span = (max(int(r["End_Timestamp"]) for r in seq) - int(seq[0]["Start_Timestamp"])) / 1e3
 tot = {}
 for r in seq:
