@@ -264,7 +264,8 @@ __global__ __launch_bounds__(1024) void k_csr_rows(int32_t N, int64_t Wb,
 // Tiles of 1,024 threads x up to 64 lengths; a thread's run is loaded with
 // independent 16-B loads into registers (one memory latency, not one per
 // length: 45 -> ~8 us per launch at 50k nodes), block scan, running carry.
-// (Staging the lengths through LDS instead: 9 vs 7 us at 10k nodes.)
+// (Staging the lengths through LDS instead: 9 vs 7 us at 10k nodes, also
+// with coalesced output stores from LDS-held offsets: 9 us, config #5 neutral.)
 constexpr int kScanPer = 64;  // lengths per thread and tile
 __global__ __launch_bounds__(1024) void k_csr_scan(int32_t N, const int32_t *__restrict__ cnt,
                                                    int32_t *__restrict__ seg_start,
