@@ -118,9 +118,9 @@ static int ensure_nodes(kp_ctx *c, int32_t N, int32_t D) {
   KP_TRY(dalloc(&c->d.seg_end, (size_t)n));
   KP_TRY(dalloc(&c->d.roff, (size_t)n + 1));
   KP_TRY(dalloc(&c->d.node_flag, (size_t)n));
-  // +4: k_accept's list mode reads node_list[wave] for up to 3 padding waves
-  KP_TRY(dalloc(&c->d.node_list, (size_t)n + 4));
-  KP_TRY(dalloc(&c->d.nrec, (size_t)n + 4));
+  // +16: k_accept's list mode reads a record for up to KP_ACC_WPB - 1 padding waves
+  KP_TRY(dalloc(&c->d.node_list, (size_t)n + 16));
+  KP_TRY(dalloc(&c->d.nrec, (size_t)n + 16));
   KP_TRY(dalloc(&c->d.nst, (size_t)n * 16));
   KP_TRY(dalloc(&c->d.perm, (size_t)n));
   c->cap_N = n;

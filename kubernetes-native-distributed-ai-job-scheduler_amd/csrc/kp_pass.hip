@@ -49,6 +49,13 @@
 #ifndef KP_GANG_PRE
 #define KP_GANG_PRE 8  // gang parts prefetched with the arrival ticket (4: +1.4 ms, 8: -0.8 ms vs none)
 #endif
+#ifndef KP_PLAN_WPB
+#define KP_PLAN_WPB 4  // k_plan waves per workgroup
+#endif
+#ifndef KP_ACC_WPB
+#define KP_ACC_WPB 1  // k_accept waves per workgroup (1 vs 4: -0.2 ms per config #3 solve)
+#endif
+static_assert(KP_ACC_WPB >= 1 && KP_ACC_WPB <= 16, "node records carry 16 spare entries");
 #ifndef KP_ACC_FLAG_FIRST
 #define KP_ACC_FLAG_FIRST 0
 #endif
@@ -625,11 +632,11 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
 }
 
 template <int D, int G, bool W32>
-__global__ __launch_bounds__(256) void k_plan(PlanArgs pa) {
+__global__ __launch_bounds__(64 * KP_PLAN_WPB) void k_plan(PlanArgs pa) {
   if (pa.pass == 0 && pa.csr_count) {
     // window w = this wave (the grid has >= ceil(A*K/64) waves): the smallest
     // request per dim over its entries, a lower bound for k_accept's pruning
-    const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int w = blockIdx.x * KP_PLAN_WPB + (threadIdx.x >> 6);
     if (w < pa.nwin) {  // wave-uniform
       const int64_t e = (int64_t)w * 64 + (threadIdx.x & 63);
       const bool ok = e < *pa.ptot;
@@ -648,12 +655,12 @@ __global__ __launch_bounds__(256) void k_plan(PlanArgs pa) {
     // the round's node records {node, seg_start, seg_end}: accept then finds
     // a node's bidder row with its first load (one thread per list entry; the
     // grid has >= A*K >= list-count threads)
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int i = blockIdx.x * (64 * KP_PLAN_WPB) + threadIdx.x;
     const int32_t cnt = *pa.nl_count;
     const int32_t n = i < pa.sp.N ? pa.node_list[i] : 0;
     if (i < cnt) pa.nrec[i] = make_int4(n, pa.seg_start[n], pa.seg_end[n], 0);
   }
-  plan_wave<D, G, W32>(pa, pa.pass, blockIdx.x * 4 + (threadIdx.x >> 6));
+  plan_wave<D, G, W32>(pa, pa.pass, blockIdx.x * KP_PLAN_WPB + (threadIdx.x >> 6));
 }
 
 // ---- accept ----------------------------------------------------------------------
@@ -954,9 +961,9 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
 // records {node, seg_start, seg_end}, written by plan pass 0) or every node;
 // nothing to do after a pass without proposals.
 template <int D, bool N32>
-__global__ __launch_bounds__(256) void k_accept(AccArgs ac, int32_t pass, int32_t use_list) {
-  const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int nw = gridDim.x * 4;  // grid-stride: the grid may be smaller than the node count
+__global__ __launch_bounds__(64 * KP_ACC_WPB) void k_accept(AccArgs ac, int32_t pass, int32_t use_list) {
+  const int wv = blockIdx.x * KP_ACC_WPB + (threadIdx.x >> 6);
+  const int nw = gridDim.x * KP_ACC_WPB;  // grid-stride: the grid may be smaller than the node count
   const int32_t pf = ac.pass_flag[pass];
   if (use_list) {  // first record and count loaded together (nrec has 4 spare entries)
 #if KP_NREC
@@ -1090,14 +1097,14 @@ struct PlanL {
     const bool w32 = c->fits32 && plan_key_ok(sp, sp.n_cand <= 16 ? 4 : 5);
     if (sp.n_cand <= 16) {
       if (w32)
-        hipLaunchKernelGGL((k_plan<D, 16, true>), dim3(blocks(A, 4 * 4)), dim3(256), 0, c->stream, pa);
+        hipLaunchKernelGGL((k_plan<D, 16, true>), dim3(blocks(A, 4 * KP_PLAN_WPB)), dim3(64 * KP_PLAN_WPB), 0, c->stream, pa);
       else
-        hipLaunchKernelGGL((k_plan<D, 16, false>), dim3(blocks(A, 4 * 4)), dim3(256), 0, c->stream, pa);
+        hipLaunchKernelGGL((k_plan<D, 16, false>), dim3(blocks(A, 4 * KP_PLAN_WPB)), dim3(64 * KP_PLAN_WPB), 0, c->stream, pa);
     } else {
       if (w32)
-        hipLaunchKernelGGL((k_plan<D, 32, true>), dim3(blocks(A, 4 * 2)), dim3(256), 0, c->stream, pa);
+        hipLaunchKernelGGL((k_plan<D, 32, true>), dim3(blocks(A, 2 * KP_PLAN_WPB)), dim3(64 * KP_PLAN_WPB), 0, c->stream, pa);
       else
-        hipLaunchKernelGGL((k_plan<D, 32, false>), dim3(blocks(A, 4 * 2)), dim3(256), 0, c->stream, pa);
+        hipLaunchKernelGGL((k_plan<D, 32, false>), dim3(blocks(A, 2 * KP_PLAN_WPB)), dim3(64 * KP_PLAN_WPB), 0, c->stream, pa);
     }
     KP_HIP(hipGetLastError());
     return KP_OK;
@@ -1116,10 +1123,10 @@ struct AcceptL {
     if (c->acc_waves > 0) waves = std::min<int64_t>(waves, c->acc_waves);
     // 32-bit first-fit sums while every capacity < 2^26 (64 terms stay < 2^32)
     if (c->fits32 && c->max_cap < ((int64_t)1 << 26))
-      hipLaunchKernelGGL((k_accept<D, true>), dim3(blocks(waves, 4)), dim3(256), 0, c->stream, ac,
+      hipLaunchKernelGGL((k_accept<D, true>), dim3(blocks(waves, KP_ACC_WPB)), dim3(64 * KP_ACC_WPB), 0, c->stream, ac,
                          pass, use_list);
     else
-      hipLaunchKernelGGL((k_accept<D, false>), dim3(blocks(waves, 4)), dim3(256), 0, c->stream, ac,
+      hipLaunchKernelGGL((k_accept<D, false>), dim3(blocks(waves, KP_ACC_WPB)), dim3(64 * KP_ACC_WPB), 0, c->stream, ac,
                          pass, use_list);
     KP_HIP(hipGetLastError());
     return KP_OK;
