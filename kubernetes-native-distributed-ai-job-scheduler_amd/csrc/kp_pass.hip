@@ -56,6 +56,9 @@
 #define KP_ACC_WPB 1  // k_accept waves per workgroup (1 vs 4: -0.2 ms per config #3 solve)
 #endif
 static_assert(KP_ACC_WPB >= 1 && KP_ACC_WPB <= 16, "node records carry 16 spare entries");
+#ifndef KP_ROWS_WPB
+#define KP_ROWS_WPB 16  // k_csr_rows rows (waves) per workgroup
+#endif
 #ifndef KP_ACC_FLAG_FIRST
 #define KP_ACC_FLAG_FIRST 0
 #endif
@@ -236,12 +239,12 @@ __global__ void k_csr_finish(int32_t P, int32_t N, int32_t K, int32_t D, int32_t
 // round for rows + scan: a last-workgroup-done scan inside k_csr_rows needs a
 // device-scope fence per wave, 150-280 us per launch; a decoupled look-back
 // over the 16-row blocks, 16 us per launch.)
-__global__ __launch_bounds__(1024) void k_csr_rows(int32_t N, int64_t Wb,
+__global__ __launch_bounds__(64 * KP_ROWS_WPB) void k_csr_rows(int32_t N, int64_t Wb,
                                                    uint32_t *__restrict__ bm,
                                                    uint2 *__restrict__ rowinfo,
                                                    int32_t *__restrict__ cnt) {
   const int lane = threadIdx.x & 63;
-  const int n = blockIdx.x * 16 + (threadIdx.x >> 6);
+  const int n = blockIdx.x * KP_ROWS_WPB + (threadIdx.x >> 6);
   if (n >= N) return;  // wave-uniform
   const int64_t rb = (int64_t)n * Wb;
   int32_t tot = 0;
@@ -1248,7 +1251,8 @@ int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev) {
   }
   if (P == 0) return KP_OK;
   if (c->csr_mode) {
-    hipLaunchKernelGGL(k_csr_rows, dim3((unsigned)((c->N + 15) / 16)), dim3(1024), 0, c->stream,
+    hipLaunchKernelGGL(k_csr_rows, dim3((unsigned)((c->N + KP_ROWS_WPB - 1) / KP_ROWS_WPB)),
+                       dim3(64 * KP_ROWS_WPB), 0, c->stream,
                        c->N, Wb, c->d.bm, c->d.rowinfo, c->d.cnt);
     KP_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_csr_scan, dim3(1), dim3(1024), 0, c->stream, c->N, c->d.cnt,

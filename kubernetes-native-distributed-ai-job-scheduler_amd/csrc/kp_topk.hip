@@ -65,6 +65,10 @@ namespace kp {
 namespace {
 using namespace dev;
 
+#ifndef KP_MERGE_WPB
+#define KP_MERGE_WPB 4  // k_merge_tour rows (waves) per workgroup
+#endif
+constexpr int kMergeWPB = KP_MERGE_WPB;
 constexpr int kFzWaves = 8;
 constexpr int kFzBS = 64 * kFzWaves;
 constexpr int kFzTile = 128 * kFzWaves;  // columns per workgroup (2 per lane)
@@ -545,7 +549,7 @@ __device__ __forceinline__ void round_keys_init(const RoundKeys &rk, int64_t t) 
 }
 
 template <int LPL>
-__global__ __launch_bounds__(256) void k_merge_tour(ScoreParams sp, const uint64_t *__restrict__ part,
+__global__ __launch_bounds__(64 * KP_MERGE_WPB) void k_merge_tour(ScoreParams sp, const uint64_t *__restrict__ part,
                                                     int32_t ntiles,
                                                     const int32_t *__restrict__ rows_unit,
                                                     const uint32_t *__restrict__ salt, int32_t rows,
@@ -554,12 +558,12 @@ __global__ __launch_bounds__(256) void k_merge_tour(ScoreParams sp, const uint64
                                                     int32_t *__restrict__ cand, RoundKeys rk) {
   extern __shared__ uint64_t slist[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int rblocks = (rows + 3) / 4;
+  const int rblocks = (rows + kMergeWPB - 1) / kMergeWPB;
   if ((int)blockIdx.x >= rblocks) {  // rk.enabled: the extra workgroups
-    round_keys_init(rk, (int64_t)(blockIdx.x - rblocks) * 256 + threadIdx.x);
+    round_keys_init(rk, (int64_t)(blockIdx.x - rblocks) * (64 * kMergeWPB) + threadIdx.x);
     return;
   }
-  const int row = blockIdx.x * 4 + wave;
+  const int row = blockIdx.x * kMergeWPB + wave;
   if (row >= rows || (rows_dev && row >= *rows_dev)) return;  // wave-uniform, no barrier below
   const int K = sp.n_cand, M = ntiles * K;
   uint64_t *L = slist + (int64_t)wave * M;
@@ -642,10 +646,10 @@ struct TopkL {
     const int M = ntiles * sp.n_cand;
     RoundKeys rk{};
     if (c->keys_in_merge) rk = round_keys_args(c, rows, sp.n_cand, rows_dev);
-    const dim3 mg(blocks(rows, 4) + (rk.enabled ? blocks(rk.init_n, 256) : 0));
-    const size_t lds = (size_t)4 * M * sizeof(uint64_t);  // <= 64 KB (M <= 2,048)
+    const dim3 mg(blocks(rows, kMergeWPB) + (rk.enabled ? blocks(rk.init_n, 64 * kMergeWPB) : 0));
+    const size_t lds = (size_t)kMergeWPB * M * sizeof(uint64_t);  // <= 16 KB per row (M <= 2,048)
 #define KP_MG(LPL)                                                                       \
-  hipLaunchKernelGGL((k_merge_tour<LPL>), mg, dim3(256), lds, c->stream, sp, c->d.part, \
+  hipLaunchKernelGGL((k_merge_tour<LPL>), mg, dim3(64 * kMergeWPB), lds, c->stream, sp, c->d.part, \
                      ntiles, rows_unit, c->d.salt, rows, rows_dev, c->d.perm, cand, rk)
     if (ntiles <= 64)
       KP_MG(1);
