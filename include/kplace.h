@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 3
+#define KP_ABI_VERSION 4  /* 4: kp_last_error_r */
 
 /* ---- limits ------------------------------------------------------------ */
 #define KP_MAX_DIMS 8       /* resource dimensions per job/node               */
@@ -164,9 +164,14 @@ void kp_destroy(kp_ctx *ctx);
 /* Generic text of an error code (static storage). */
 const char *kp_strerror(int code);
 /* Detailed text of the last error returned on this context (the HIP/RCCL
-   call and its message), "" if none. Valid until the next call on ctx; safe
-   from any OS thread (kept per context, not per thread). */
+   call and its message), "" if none. Kept per context, not per thread (cgo
+   hops OS threads). The pointer stays valid for the context's lifetime; a
+   later failing call on ctx may overwrite the text while it is read, so a
+   caller with concurrent calls on one context uses kp_last_error_r. */
 const char *kp_last_error(kp_ctx *ctx);
+/* The same text copied into buf (NUL-terminated, truncated to len - 1 bytes)
+   under the context lock. Returns the full length of the message. */
+int kp_last_error_r(kp_ctx *ctx, char *buf, size_t len);
 int kp_abi_version(void);
 /* Writes the 128-byte RCCL unique id for a multi-process context. */
 int kp_dist_unique_id(void *out128);

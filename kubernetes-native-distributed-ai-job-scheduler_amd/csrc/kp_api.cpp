@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <thread>
 
 #include "kp_internal.hpp"
 
@@ -57,6 +58,13 @@ struct Entry {
   }
   ~Entry() { g_cur = prev; }
 };
+
+// KP_DEBUG_KNOBS=1 is the only environment variable the product reads; the
+// tuning / A/B / test knobs below it are ignored without it
+static const char *knob(const char *name) {
+  const char *on = std::getenv("KP_DEBUG_KNOBS");
+  return on && std::strcmp(on, "1") == 0 ? std::getenv(name) : nullptr;
+}
 
 static int fail(int code, const char *fmt, ...) {
   char buf[256];
@@ -314,26 +322,31 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   c->world = world;
   c->rank = rank;
   c->max_pairs_matrix = max_pairs;
-  if (const char *e = std::getenv("KP_SELECT_LDS_CAP")) c->select_lds_cap = std::atoi(e);
-  if (const char *e = std::getenv("KP_SELECT_GENERIC")) c->select_generic = std::atoi(e) != 0;
-  if (const char *e = std::getenv("KP_SELECT_BS")) c->select_bs = std::atoi(e);
-  if (const char *e = std::getenv("KP_SCORE_WG_TARGET")) c->score_wg_target = std::max(64, std::atoi(e));
-  if (const char *e = std::getenv("KP_SCORE_MIN_RPB")) c->score_min_rpb = std::max(1, std::atoi(e));
-  if (const char *e = std::getenv("KP_SCORE_NPL")) c->score_npl = std::atoi(e) == 4 ? 4 : 2;
-  if (const char *e = std::getenv("KP_COMPACT_MAX")) c->compact_max = std::atoi(e);
-  if (const char *e = std::getenv("KP_FUSED")) c->fused_enabled = std::atoi(e) != 0;
-  if (const char *e = std::getenv("KP_ACC_LIST")) c->acc_list = std::atoi(e);
-  if (const char *e = std::getenv("KP_KEYS_MERGE")) c->keys_merge_enabled = std::atoi(e) != 0;
-  if (const char *e = std::getenv("KP_ROUND_BEGIN")) c->round_begin = std::atoi(e) != 0;
-  if (const char *e = std::getenv("KP_CSR_SORT")) c->csr_count_enabled = std::atoi(e) == 0;
-  if (const char *e = std::getenv("KP_CSR_BM_MAX")) c->csr_bm_max = std::atoll(e);
-  if (const char *e = std::getenv("KP_ACC_WAVES")) c->acc_waves = std::max(0, std::atoi(e));
-  if (const char *e = std::getenv("KP_FZ_WG_TARGET")) c->fz_wg_target = std::max(64, std::atoi(e));
-  if (const char *e = std::getenv("KP_COUNT_DIRECT")) c->count_direct = std::atoi(e) != 0;
-  if (const char *e = std::getenv("KP_HOST_PROF")) c->host_prof = std::atoi(e) != 0;
-  if (const char *e = std::getenv("KP_FZ_H16")) c->fz_h16 = std::atoi(e) != 0;
-  if (const char *e = std::getenv("KP_FZ_TIE_BITS")) c->fz_tie_bits = std::max(0, std::min(31, std::atoi(e)));
-  if (const char *e = std::getenv("KP_FZ_PROF"))  // phase clocks (KP_FZ_PROFILE builds only)
+  // A/B and test knobs: honoured only under KP_DEBUG_KNOBS=1, so that a
+  // manager process's inherited environment cannot switch kernels or key
+  // encodings; the defaults below are the product
+  if (const char *e = knob("KP_SELECT_LDS_CAP")) c->select_lds_cap = std::atoi(e);
+  if (const char *e = knob("KP_SELECT_GENERIC")) c->select_generic = std::atoi(e) != 0;
+  if (const char *e = knob("KP_SELECT_BS")) c->select_bs = std::atoi(e);
+  if (const char *e = knob("KP_SCORE_WG_TARGET")) c->score_wg_target = std::max(64, std::atoi(e));
+  if (const char *e = knob("KP_SCORE_MIN_RPB")) c->score_min_rpb = std::max(1, std::atoi(e));
+  if (const char *e = knob("KP_SCORE_NPL")) c->score_npl = std::atoi(e) == 4 ? 4 : 2;
+  if (const char *e = knob("KP_COMPACT_MAX")) c->compact_max = std::atoi(e);
+  if (const char *e = knob("KP_FUSED")) c->fused_enabled = std::atoi(e) != 0;
+  if (const char *e = knob("KP_ACC_LIST")) c->acc_list = std::atoi(e);
+  if (const char *e = knob("KP_KEYS_MERGE")) c->keys_merge_enabled = std::atoi(e) != 0;
+  if (const char *e = knob("KP_ROUND_BEGIN")) c->round_begin = std::atoi(e) != 0;
+  if (const char *e = knob("KP_CSR_SORT")) c->csr_count_enabled = std::atoi(e) == 0;
+  if (const char *e = knob("KP_CSR_BM_MAX")) c->csr_bm_max = std::atoll(e);
+  if (const char *e = knob("KP_ACC_WAVES")) c->acc_waves = std::max(0, std::atoi(e));
+  if (const char *e = knob("KP_FZ_WG_TARGET")) c->fz_wg_target = std::max(64, std::atoi(e));
+  if (const char *e = knob("KP_COUNT_DIRECT")) c->count_direct = std::atoi(e) != 0;
+  if (const char *e = knob("KP_HOST_PROF")) c->host_prof = std::atoi(e) != 0;
+  if (const char *e = knob("KP_FZ_H16")) c->fz_h16 = std::atoi(e) != 0;
+  if (const char *e = knob("KP_TEST_FAIL_SOLVE"))  // tests: rank e fails its next solve
+    c->test_fail_solve = world > 1 && std::atoi(e) == rank;
+  if (const char *e = knob("KP_FZ_TIE_BITS")) c->fz_tie_bits = std::max(0, std::min(31, std::atoi(e)));
+  if (const char *e = knob("KP_FZ_PROF"))  // phase clocks (KP_FZ_PROFILE builds only)
     if (std::atoi(e) != 0 && hipMalloc(reinterpret_cast<void **>(&c->d.fz_prof), kProfWords * 8) == hipSuccess) {
       // [16 + 64 + 4 L + {0, 2}]: minima of the pass-profile launch stamps
       std::vector<uint64_t> h(kProfWords, 0);
@@ -639,6 +652,36 @@ static int load_jobs_impl(kp_ctx *c, int32_t J, const int64_t *req, const int32_
   return KP_OK;
 }
 
+// Waits of a multi-rank solve. A shard of kp_create_multi polls instead of
+// blocking, so that a peer shard that failed (and so never joins the next
+// collective, whose kernels would then wait for it forever) releases it: the
+// multi context aborts the communicators once every shard has returned.
+static int wait_event(kp_ctx *c, hipEvent_t ev) {
+  if (!c->peer_failed) {
+    KP_HIP(hipEventSynchronize(ev));
+    return KP_OK;
+  }
+  for (uint32_t spin = 0;; ++spin) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e == hipSuccess) return KP_OK;
+    if (e != hipErrorNotReady) {
+      kp_set_error("hipEventQuery", e);
+      return KP_EHIP;
+    }
+    if (c->peer_failed->load(std::memory_order_acquire))
+      return fail(KP_ERCCL, "kp_solve: a peer shard failed; the exchange cannot complete");
+    if (spin < 256)
+      std::this_thread::yield();
+    else
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
+static int wait_stream(kp_ctx *c, hipEvent_t ev) {
+  KP_HIP(hipEventRecord(ev, c->stream));
+  return wait_event(c, ev);
+}
+
 // ---------------------------------------------------------------------------
 // This rank's candidates -> every rank's, as fixed-size blocks
 // [count, (unit, K candidates) x B] (B: the same slot bound on every rank), so
@@ -650,6 +693,9 @@ static int exchange_round(kp_ctx *c, int32_t B, int32_t K) {
   const size_t per = 1 + (size_t)B * (K + 1);
   KP_TRY(launch_pack_exchange(c, B, K));
   if (c->nccl_comm) {
+    if (c->peer_failed && c->peer_failed->load(std::memory_order_acquire))
+      return fail(KP_ERCCL, "kp_solve: a peer shard failed before the exchange");
+    c->in_collective = true;
     if (ncclAllGather(c->d.xg_send, c->d.xg_recv, per, ncclInt32,
                       static_cast<ncclComm_t>(c->nccl_comm), c->stream) != ncclSuccess)
       return fail(KP_ERCCL, "ncclAllGather of %zu ints", per);
@@ -684,6 +730,9 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     return fail(KP_ESTATE, "kp_solve: multi-rank context without an exchange");
   KP_TRY(check_params(p, c->D));
   c->solved = false;
+  // per-solve state that an earlier failed solve may have left set
+  c->keys_in_merge = false;
+  c->in_collective = false;
   KP_HIP(hipSetDevice(c->device));
   const ScoreParams sp = make_sp(c, p);
   const int32_t K = p->n_cand, U = c->U, N = c->N;
@@ -886,11 +935,14 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     // ranks, so every rank calls the all-gather with the same size).
     hipEvent_t evG;
     KP_TRY(E.make(&evG, hipEventDisableTiming));
+    hipEvent_t evS;
+    KP_TRY(E.make(&evS, hipEventDisableTiming));
     int32_t *Al_h = c->pinned + 256, *G_h = c->pinned + 320;
     int64_t Smax = 0;  // largest shard
     for (int r = 0; r < c->world; ++r)
       Smax = std::max<int64_t>(Smax, (int64_t)U * (r + 1) / c->world - (int64_t)U * r / c->world);
     const bool chunked = std::min<int64_t>(shard, Smax) > rpc;
+    KP_TRY(csr_reserve(c, U));  // no reallocation between the round's collectives
     int64_t G_bound = U;
     for (int32_t r = 0; G_bound > 0; ++r) {
       if (p->max_rounds > 0 && r >= p->max_rounds) break;
@@ -903,11 +955,15 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
       }
       const int32_t rows = (int32_t)std::min<int64_t>(shard, B);
       if (chunked) {  // the score matrix is chunked: needs the exact local count
-        KP_HIP(hipStreamSynchronize(c->stream));
+        KP_TRY(wait_stream(c, evS));
         for (int64_t r0 = 0; r0 < *Al_h; r0 += rpc)
           KP_TRY(score_select(r0, (int32_t)std::min<int64_t>(rpc, *Al_h - r0), nullptr, r));
       } else if (rows > 0) {
         KP_TRY(score_select(0, rows, c->d.counters, r));
+      }
+      if (c->test_fail_solve) {  // test knob: this rank never reaches the exchange
+        c->test_fail_solve = 0;
+        return fail(KP_ENOMEM, "KP_TEST_FAIL_SOLVE: injected failure of rank %d before its exchange", c->rank);
       }
       KP_TRY(exchange_round(c, B, K));
       KP_HIP(hipMemcpyAsync(G_h, c->d.counters + 1, sizeof(int32_t), hipMemcpyDeviceToHost,
@@ -915,7 +971,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
       KP_HIP(hipEventRecord(evG, c->stream));
       KP_TRY(passes_of_round((int32_t)std::min<int64_t>(U, (int64_t)B * c->world),
                              c->d.counters + 1));
-      KP_HIP(hipEventSynchronize(evG));  // lands before this round's passes run
+      KP_TRY(wait_event(c, evG));  // lands before this round's passes run
       round_active.push_back(*Al_h);
       G_bound = *G_h;
     }
@@ -933,7 +989,14 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
                           c->stream));
   SolveStats dst{};
   KP_HIP(hipMemcpyAsync(&dst, c->d.stats, sizeof dst, hipMemcpyDeviceToHost, c->stream));
-  KP_HIP(hipStreamSynchronize(c->stream));
+  if (c->world > 1) {
+    hipEvent_t evF;
+    KP_TRY(E.make(&evF, hipEventDisableTiming));
+    KP_TRY(wait_stream(c, evF));
+  } else {
+    KP_HIP(hipStreamSynchronize(c->stream));
+  }
+  c->in_collective = false;  // every collective of this solve completed
   const int32_t rounds = (int32_t)dst.rounds, passes = (int32_t)dst.passes;
   const int64_t pairs = dst.active_sum * N;
   tm.solve_ms = ev_ms(t0, t1);
@@ -1048,7 +1111,25 @@ const char *kp_strerror(int code) {
 const char *kp_last_error(kp_ctx *c) {
   if (!c) return "";
   std::lock_guard<std::mutex> g(c->mu);
-  return c->last_error.c_str();
+  // a copy in storage owned by the context: never freed by a later call
+  const size_t n = std::min(c->last_error.size(), sizeof c->last_error_buf - 1);
+  std::memcpy(c->last_error_buf, c->last_error.data(), n);
+  c->last_error_buf[n] = '\0';
+  return c->last_error_buf;
+}
+
+int kp_last_error_r(kp_ctx *c, char *buf, size_t len) {
+  if (!c) {
+    if (buf && len) buf[0] = '\0';
+    return 0;
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  if (buf && len) {
+    const size_t n = std::min(c->last_error.size(), len - 1);
+    std::memcpy(buf, c->last_error.data(), n);
+    buf[n] = '\0';
+  }
+  return (int)std::min<size_t>(c->last_error.size(), INT32_MAX);
 }
 
 int kp_dist_unique_id(void *out128) {
@@ -1092,7 +1173,7 @@ void kp_destroy(kp_ctx *c) {
   if (d.fz_prof) {  // KP_FZ_PROF: the accumulated phase clocks
     std::vector<uint64_t> h(kProfWords, 0);
     if (hipMemcpy(h.data(), d.fz_prof, kProfWords * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-      if (std::getenv("KP_PASS_SPANS"))
+      if (knob("KP_PASS_SPANS"))
         for (int L = 0; L < 1024; ++L) {
           const uint64_t *x = h.data() + 16 + 64 + 4 * L;
           if (x[0] == ~0ull || x[2] == ~0ull) continue;

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <functional>
 #include <mutex>
@@ -162,6 +163,14 @@ struct kp_ctx {
   kp_allgather_fn allgather = nullptr;
   void *allgather_user = nullptr;
   std::vector<int32_t> h_xg_send, h_xg_recv;
+  // kp_create_multi shard: set by the multi context when a peer shard's call
+  // failed; the shard's waits on its exchange poll it instead of blocking, so a
+  // peer that never joins a collective cannot hang this shard
+  const std::atomic<int> *peer_failed = nullptr;
+  bool in_collective = false;  // this solve enqueued an RCCL collective
+  // KP_TEST_FAIL_SOLVE (test knob): the next solve on this rank fails with
+  // KP_ENOMEM at its first exchange (the peer-failure path of kp_create_multi)
+  int32_t test_fail_solve = 0;
   int64_t max_pairs_matrix = 0;
   hipStream_t stream = nullptr;
   bool profiling = false;
@@ -244,6 +253,9 @@ struct kp_ctx {
   kp_result last{};
   kp_timing timing{};
   std::string last_error;  // detail of the last failed call (kp_last_error)
+  // what kp_last_error returns: a copy of last_error taken under the lock,
+  // in storage that later calls overwrite but never free
+  char last_error_buf[512] = {0};
 };
 
 // Kernel launchers (kp_score.hip, kp_pass.hip).
@@ -270,6 +282,7 @@ int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev = nul
 // this round's index form (counting or sort) and its bitmap; called by
 // launch_csr_build, or before the candidate merge when that does k_csr_keys' work
 int csr_prepare(kp_ctx *c, int32_t A, int32_t K);
+int csr_reserve(kp_ctx *c, int32_t Amax);
 RoundKeys round_keys_args(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev);
 int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass,
                 const int32_t *A_dev = nullptr);

@@ -96,6 +96,10 @@ struct Multi {
   std::vector<RankRef> refs;
   bool rccl = false;
   bool broken = false;  // an RCCL shard failed mid-exchange: communicators aborted
+  // set by the first shard whose call fails (its index in first_fail): the
+  // other shards' exchange waits poll it and return instead of hanging
+  std::atomic<int> failed{0};
+  std::atomic<int> first_fail{-1};
 };
 
 static void worker_loop(Worker *w, int device) {
@@ -126,6 +130,8 @@ int multi_run(kp_ctx *c, const std::function<int(kp_ctx *, int)> &fn, bool all) 
     return KP_ERCCL;
   }
   if (M.inproc) M.inproc->reset();
+  M.failed.store(0);
+  M.first_fail.store(-1);
   const int n = all ? (int)M.shards.size() : 1;
   for (int i = 0; i < n; ++i) {
     Worker &w = *M.workers[i];
@@ -133,26 +139,40 @@ int multi_run(kp_ctx *c, const std::function<int(kp_ctx *, int)> &fn, bool all) 
     std::lock_guard<std::mutex> lk(w.m);
     w.job = [&fn, sh, i, &M]() {
       const int rc = fn(sh, i);
-      if (rc != KP_OK && M.inproc) M.inproc->poison();  // release the others
+      if (rc != KP_OK) {  // release the others at once (not after every shard returned)
+        int none = -1;
+        M.first_fail.compare_exchange_strong(none, i);
+        M.failed.store(1, std::memory_order_release);
+        if (M.inproc) M.inproc->poison();
+      }
       return rc;
     };
     w.done = false;
     w.has = true;
     w.cv.notify_all();
   }
-  int rc = KP_OK;
+  std::vector<int> rcs(n, KP_OK);
   for (int i = 0; i < n; ++i) {
     Worker &w = *M.workers[i];
     std::unique_lock<std::mutex> lk(w.m);
     w.cv.wait(lk, [&] { return w.done; });
-    if (w.rc != KP_OK && rc == KP_OK) {
-      rc = w.rc;
-      std::lock_guard<std::mutex> sg(M.shards[i]->mu);
-      c->last_error = "shard " + std::to_string(i) + ": " + M.shards[i]->last_error;
-    }
+    rcs[i] = w.rc;
   }
-  if (rc != KP_OK && M.rccl && all && n > 1 && (rc == KP_EHIP || rc == KP_ERCCL)) {
-    // a shard may have left its peers inside a collective: abort them all
+  // report the root cause: the shard that failed first (its peers then fail
+  // with KP_ERCCL "a peer shard failed")
+  const int f = M.first_fail.load();
+  if (f < 0) return KP_OK;
+  const int rc = rcs[f];
+  {
+    std::lock_guard<std::mutex> sg(M.shards[f]->mu);
+    c->last_error = "shard " + std::to_string(f) + ": " + M.shards[f]->last_error;
+  }
+  bool stuck = false;  // some shard has a collective in flight that may never complete
+  for (int i = 0; i < n; ++i) stuck = stuck || M.shards[i]->in_collective;
+  if (M.rccl && all && n > 1 && stuck) {
+    // every worker has returned (no host thread is inside RCCL): abort the
+    // communicators so that device-side collectives waiting for the failed
+    // shard terminate; the context then reports KP_ERCCL for every call
     for (kp_ctx *sh : M.shards)
       if (sh->nccl_comm) (void)ncclCommAbort(static_cast<ncclComm_t>(sh->nccl_comm));
     for (kp_ctx *sh : M.shards) sh->nccl_comm = nullptr;
@@ -218,6 +238,7 @@ int multi_create(kp_ctx **out, const int32_t *ids, int32_t n, int64_t max_pairs)
         if (comms[k]) ncclCommDestroy(comms[k]);
       break;
     }
+    sh->peer_failed = &M.failed;
     if (M.inproc) {
       M.refs[i] = RankRef{M.inproc.get(), i};
       sh->allgather = inproc_allgather;

@@ -1194,6 +1194,17 @@ static int ensure_bitmap(kp_ctx *c, int64_t words) {
   return KP_OK;
 }
 
+// the bitmap every counting-mode round of up to Amax slots can use, allocated
+// up front (a multi-rank solve: no hipFree, which waits for the whole device,
+// between its collectives)
+int csr_reserve(kp_ctx *c, int32_t Amax) {
+  if (!c->csr_count_enabled || Amax <= 0 || c->N <= 0) return KP_OK;
+  const int64_t words = std::min<int64_t>((int64_t)c->N * (((int64_t)Amax + 31) / 32), c->csr_bm_max);
+  if (c->d.bm && words <= c->cap_bm_words && c->N <= c->cap_cnt_N) return KP_OK;
+  const int rc = ensure_bitmap(c, words);
+  return rc == KP_ENOMEM ? KP_OK : rc;  // out of memory: rounds fall back to the sort
+}
+
 int csr_prepare(kp_ctx *c, int32_t A, int32_t K) {
   const int64_t P = (int64_t)A * K;
   const int64_t Wb = ((int64_t)A + 31) / 32;

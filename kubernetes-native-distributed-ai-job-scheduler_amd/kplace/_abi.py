@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-KP_ABI_VERSION = 3
+KP_ABI_VERSION = 4
 KP_MAX_DIMS = 8
 KP_MAX_CAND = 32
 KP_MAX_GANG = 64
@@ -160,6 +160,7 @@ def load_library(path: str | None = None) -> C.CDLL:
         "kp_create": (C.c_int, [C.POINTER(vp), C.POINTER(Config)]),
         "kp_create_multi": (C.c_int, [C.POINTER(vp), _i32p, C.c_int32, C.POINTER(Config)]),
         "kp_last_error": (C.c_char_p, [vp]),
+        "kp_last_error_r": (C.c_int, [vp, C.c_char_p, C.c_size_t]),
         "kp_destroy": (None, [vp]),
         "kp_strerror": (C.c_char_p, [C.c_int]),
         "kp_abi_version": (C.c_int, []),
@@ -189,7 +190,7 @@ def load_library(path: str | None = None) -> C.CDLL:
 # every symbol include/kplace.h declares (tests check the export table)
 EXPORTED = (
     "kp_params_default", "kp_create", "kp_create_multi", "kp_destroy", "kp_strerror",
-    "kp_last_error",
+    "kp_last_error", "kp_last_error_r",
     "kp_abi_version", "kp_dist_unique_id", "kp_place", "kp_load_nodes",
     "kp_load_jobs", "kp_solve", "kp_fetch", "kp_apply_delta", "kp_reset_nodes", "kp_score",
     "kp_last_timing", "kp_set_profiling", "kp_parse_gpu_memory", "kp_load_running",

@@ -35,8 +35,16 @@ def _check(rc: int, where: str, h=None) -> None:
     if rc != _abi.KP_OK:
         detail = ""
         if h is not None and h.value:
-            detail = lib().kp_last_error(h).decode(errors="replace")
+            detail = last_error(h)
         raise KPlaceError(rc, where, detail)
+
+
+def last_error(h) -> str:
+    """kp_last_error_r: the context's last error text, copied under its lock
+    (safe while other threads call into the same context)."""
+    buf = C.create_string_buffer(512)
+    lib().kp_last_error_r(h, buf, len(buf))
+    return buf.value.decode(errors="replace")
 
 
 def _ptr(a, t):
@@ -105,7 +113,7 @@ class Placer:
 
     def last_error(self) -> str:
         """kp_last_error: detail of the last failed call on this context."""
-        return lib().kp_last_error(self._h).decode(errors="replace")
+        return last_error(self._h)
 
     def close(self) -> None:
         if getattr(self, "_h", None):

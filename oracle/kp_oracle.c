@@ -395,7 +395,8 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
   }
   st->pairs += (int64_t)active0 * N;
 
-  const int trace = getenv("KPO_TRACE") != NULL; /* per-round counts on stderr (analysis) */
+  const char *trace_env = getenv("KPO_TRACE"); /* per-round counts on stderr (analysis) */
+  const int trace = trace_env ? (atoi(trace_env) > 1 ? 2 : 1) : 0;
   int32_t passes0 = st->passes;
   for (int pass = 0; pass < st->p.max_passes; ++pass) {
     /* proposals of every open unit, planned against the current usage */
@@ -412,6 +413,12 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
     if (np == 0) break;
     st->passes++;
     qsort(props, np, sizeof *props, cmp_prop);
+    if (trace > 1) { /* KPO_TRACE=2: per-pass open units, proposals, bid nodes */
+      int32_t nopen = 0, nodes = 0;
+      for (int32_t u = 0; u < U; ++u) nopen += open[u];
+      for (int32_t k = 0; k < np; ++k) nodes += k == 0 || props[k].node != props[k - 1].node;
+      fprintf(stderr, "kpo pass %d.%d open %d props %d nodes %d\n", st->rounds, pass, nopen, np, nodes);
+    }
     /* per node, in unit rank order: first-fit against the remaining capacity */
     int64_t rem[KP_MAX_DIMS];
     for (int32_t i = 0; i < np;) {

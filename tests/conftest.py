@@ -9,6 +9,11 @@ for p in (PKG, os.path.join(REPO, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# The library's A/B and test knobs (KP_FUSED, KP_FZ_TIE_BITS, ...) are read
+# only under KP_DEBUG_KNOBS=1; the tests that set one exercise alternative
+# code paths on purpose (tests/test_gpu_parity.py), so the suite opts in.
+os.environ["KP_DEBUG_KNOBS"] = "1"
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 GPU (runs on the MI355X box)")

@@ -57,7 +57,7 @@ def _worker(rank, world, port, cfg, mpm, out_q):
     dist.all_gather(all_nodes, t)
     same = all(torch.equal(all_nodes[0], x) for x in all_nodes)
     if rank == 0:
-        ref = ob.place(ob.SnapshotBuf.from_workload(w), p, nthreads=4)
+        ref = ob.place(ob.SnapshotBuf.from_workload(w), p, nthreads=8)
         ok = same and all(np.array_equal(g[k], ref[k]) for k in ("node", "score", "status", "used"))
         out_q.put((ok, g["rounds"], ref["rounds"], g["placed"], ref["placed"]))
     dist.barrier()
@@ -70,6 +70,7 @@ def _worker(rank, world, port, cfg, mpm, out_q):
     (2, (3, 1, 64), 0),            # rank 0 holds no unit
     (3, (3, 6000, 512), 0),        # uneven shards
     (2, (3, 6000, 512), 512 * 700),  # chunked score matrix (exact local count path)
+    (2, (3, 100_000, 10_000), 0),  # BASELINE config #3 at full size (configs[2])
 ])
 def test_sharded_gpu_solve_matches_oracle(oracle, world, cfg, mpm):
     ctx = mp.get_context("spawn")

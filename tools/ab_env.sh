@@ -3,6 +3,7 @@
 # every value is run alternately, 3 times each, bench without events; with
 # EVENTS=1 also a run with per-launch HIP events (filter+score roofline fraction).
 set -o pipefail
+export KP_DEBUG_KNOBS=1  # the library reads its A/B knobs only with this set
 VAR=$1; VALS=$2
 mkdir -p gpurun_out/ab
 for i in 1 2 3; do

@@ -2,6 +2,7 @@
 #   bash tools/ab_mix.sh a_base b_variant a_base@KP_ACC_LIST=1
 # each case = build/ab/<lib>.so [@VAR=VAL[,VAR=VAL]]; bench without events.
 set -o pipefail
+export KP_DEBUG_KNOBS=1  # the library reads its A/B knobs only with this set
 mkdir -p gpurun_out/ab
 AB=kubernetes-native-distributed-ai-job-scheduler_amd/build/ab
 for i in 1 2 3; do

@@ -1,6 +1,7 @@
 # A/B of one library knob on the config #5 streaming loop (tools/stream_profile.py,
 # 40 batches), alternating: bash tools/ab_stream_env.sh KP_ACC_WAVES "0 4096 2048"
 set -o pipefail
+export KP_DEBUG_KNOBS=1  # the library reads its A/B knobs only with this set
 VAR=$1; VALS=$2
 mkdir -p gpurun_out/abs
 for i in 1 2; do

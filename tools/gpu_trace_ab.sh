@@ -1,6 +1,7 @@
 # Kernel traces of one bench solve under two env settings (A/B of a library
 # knob): gpu_trace_ab.sh "VAR=a" "VAR=b" ; per-kernel totals via ktrace_sum.py
 set -o pipefail
+export KP_DEBUG_KNOBS=1  # the library reads its A/B knobs only with this set
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 i=0
 for setting in "$@"; do
