@@ -15,9 +15,11 @@ Beside the step (same run, outside the timed steps):
                   placement latency"; the reference's analogue is
                   the reconcile histogram around Reconcile,
                   internal/controller/llmservice_controller.go:70-73);
-  config4         BASELINE config #4 (200k x 20k, 30% GPU occupancy of running
-                  jobs): solve + kp_preempt;
-  streaming       BASELINE config #5 (1M-job trace, 5k micro-batches, 50k nodes);
+  config4         BASELINE config #4 (200k x 20k, running jobs filling every
+                  dim to >= 30% of its capacity): solve + kp_preempt, with the
+                  oracle timed beside it on a stated sample;
+  streaming       BASELINE config #5 (1M-job trace, 5k micro-batches, 50k nodes),
+                  with the oracle timed beside it on the first batches;
   cpu_baseline    the CPU restatement (oracle/, test infrastructure) on the SAME
                   full config #3, on 1 thread and on every host core given to
                   this job.
@@ -148,13 +150,82 @@ def streaming(args, make_placer):
             run_node, run_job = run_node[~done], run_job[~done]
     lat_ms = np.array(lat) * 1e3
     n = len(lat)
-    return {"config": f"#5 streaming: {args.stream_jobs} jobs in {B}-job micro-batches vs "
+    cpu = None if args.no_cpu_baseline else streaming_cpu(args, cap, topo, req, prio, p)
+    return {"cpu_baseline": cpu,
+            "config": f"#5 streaming: {args.stream_jobs} jobs in {B}-job micro-batches vs "
                       f"{args.stream_nodes} nodes, 20% completions per batch",
             "batches": n, "p50_ms": float(np.percentile(lat_ms, 50)),
             "p99_ms": float(np.percentile(lat_ms, 99)), "max_ms": float(lat_ms.max()),
             "jobs_per_s": args.stream_jobs / float(np.sum(lat)), "placed_jobs": placed,
             "mean_rounds": rounds / max(n, 1),
             "mean_ms": {k: v * 1e3 / max(n, 1) for k, v in parts.items()}}
+
+
+def streaming_cpu(args, cap, topo, req, prio, p):
+    """The oracle beside the config #5 leg (bounded sample): the first
+    `--cpu-stream-batches` micro-batches replayed exactly as the GPU leg does
+    (per batch: a full placement of the batch against the resident usage,
+    then the 20% completions), on every host core and, for batch 0 only, on 1
+    thread. Per-batch wall time of the oracle call."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_bind as ob
+    B, nb = args.stream_batch, args.cpu_stream_batches
+    out = {}
+    for label, threads, batches in (("all_cores", host_cores(), nb), ("single", 1, 1)):
+        progress(f"cpu baseline (config #5): oracle, {threads} thread(s), {batches} batch(es)")
+        used = np.zeros_like(cap)
+        run_node, run_job = np.zeros(0, np.int32), np.zeros(0, np.int64)
+        per = []
+        for b in range(batches):
+            lo, hi = b * B, (b + 1) * B
+            rq = np.ascontiguousarray(req[:, lo:hi])
+            t = time.perf_counter()
+            o = ob.place(ob.SnapshotBuf(rq, cap, used, prio[lo:hi], topo=topo), p, nthreads=threads)
+            per.append(time.perf_counter() - t)
+            used = o["used"].copy()
+            ok = o["node"] >= 0
+            run_node = np.concatenate([run_node, o["node"][ok]])
+            run_job = np.concatenate([run_job, lo + np.nonzero(ok)[0]])
+            done = synth.config5_completions(b, run_job)
+            np.subtract.at(used.T, run_node[done], req[:, run_job[done]].T)
+            run_node, run_job = run_node[~done], run_job[~done]
+        out[label] = {"threads": threads, "batches": batches,
+                      "batch_ms": [1e3 * x for x in per], "jobs_per_s": B * batches / sum(per)}
+    return {"value": out["all_cores"]["jobs_per_s"], "unit": "jobs/s", "cores": host_cores(),
+            "kind": "port", "cpu_model": cpu_model(),
+            "sample": f"oracle/kp_oracle.c on the first {nb} {B}-job micro-batches of the same "
+                      f"trace (batch 0 only on 1 thread); GPU leg: all batches", **out}
+
+
+def config4_cpu(args, w, p):
+    """The oracle beside the config #4 leg (bounded sample; the full 200k x 20k
+    solve + preemption takes the oracle ~25 min on 6 cores): the first
+    `--cpu-c4-jobs` pending jobs of the same snapshot (same nodes, same
+    running jobs and usage), the first `--cpu-c4-rounds` rounds of their
+    solve, then the preemption nominations (kpo_preempt), on every host core
+    and on 1 thread. Reported as scored job-node pairs per second."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_bind as ob
+    Js = min(args.cpu_c4_jobs, w.J)
+    m = w.meta
+    sb = ob.SnapshotBuf(np.ascontiguousarray(w.req[:, :Js]), w.cap, w.used, w.prio[:Js],
+                        topo=w.topo)
+    p = _abi.default_params(**{**synth.CONFIG_PARAMS[4], "max_rounds": args.cpu_c4_rounds})
+    out = {}
+    for label, threads in (("all_cores", host_cores()), ("single", 1)):
+        progress(f"cpu baseline (config #4): oracle on {threads} thread(s), {Js} jobs")
+        t = time.perf_counter()
+        r, pr = ob.preempt(sb, p, m["run_node"], m["run_req"], m["run_prio"], nthreads=threads)
+        dt = time.perf_counter() - t
+        out[label] = {"threads": threads, "seconds": dt, "rounds": r["rounds"],
+                      "placed_jobs": r["placed"], "preemptors": pr["preemptors"],
+                      "pairs_per_s": (float(r["pairs"]) + float(pr["pairs"])) / dt}
+    return {"value": out["all_cores"]["pairs_per_s"], "unit": "pairs/s", "cores": host_cores(),
+            "kind": "port", "cpu_model": cpu_model(),
+            "sample": f"oracle/kp_oracle.c: the first {args.cpu_c4_rounds} rounds of the solve of "
+                      f"the first {Js} of the {w.J} pending jobs against the same {w.N}-node "
+                      f"snapshot and running jobs, then kpo_preempt; pairs = scored job-node "
+                      f"pairs of the solve + preemption", **out}
 
 
 def config4(args, make_placer):
@@ -181,10 +252,15 @@ def config4(args, make_placer):
                 sol.append(t1 - t0)
                 pre.append(t2 - t1)
     s_ms, p_ms = 1e3 * float(np.mean(sol)), 1e3 * float(np.mean(pre))
+    util = w.used.sum(1) / w.cap.sum(1)
+    cpu = None if args.no_cpu_baseline else config4_cpu(args, w, p)
     return {"config": f"#4 preemption: {w.J} pending x {w.N} nodes, {m['run_node'].size} running "
-                      f"jobs at {w.used[2].sum() / w.cap[2].sum():.3f} GPU occupancy",
+                      f"jobs; occupancy per dim (cpu, mem, gpu, gpu_mem) "
+                      f"{', '.join(f'{x:.3f}' for x in util)} (every dim >= 0.30)",
             "solve_ms": s_ms, "preempt_ms": p_ms,
             "pairs_per_s": float(w.J) * w.N / ((s_ms + p_ms) / 1e3),
+            "pairs_scored_per_s": (float(st["pairs"]) + float(pr["pairs"])) / ((s_ms + p_ms) / 1e3),
+            "cpu_baseline": cpu,
             "rounds": st["rounds"], "passes": st["passes"], "placed_jobs": st["placed"],
             "preemptors": pr["preemptors"], "nominated": pr["nominated"],
             "preempt_pairs": pr["pairs"], "steps": args.c4_steps}
@@ -224,6 +300,12 @@ def main():
     ap.add_argument("--c4-nodes", type=int, default=20_000)
     ap.add_argument("--c4-steps", type=int, default=3)
     ap.add_argument("--no-config4", action="store_true")
+    ap.add_argument("--cpu-c4-jobs", type=int, default=10_000,
+                    help="config #4 CPU baseline sample: the first N pending jobs")
+    ap.add_argument("--cpu-c4-rounds", type=int, default=2,
+                    help="config #4 CPU baseline sample: rounds of their solve")
+    ap.add_argument("--cpu-stream-batches", type=int, default=2,
+                    help="config #5 CPU baseline sample: the first N micro-batches")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="time the steps without per-launch HIP events (no roofline)")
     args = ap.parse_args()

@@ -271,7 +271,7 @@ typedef struct kp_timing {
   int64_t select_bytes;     /* algorithmic bytes of the select kernels       */
   int32_t fused;            /* 1: fused filter+score+top-K (no score matrix;
                                score_* then time/count k_score_topk)         */
-  int32_t reserved;
+  int32_t loop_rounds;      /* rounds whose passes ran as one persistent launch */
 } kp_timing;
 int kp_last_timing(kp_ctx *ctx, kp_timing *t);
 

@@ -189,7 +189,8 @@ static int ensure_units(kp_ctx *c, int32_t U, int32_t J) {
     KP_TRY(dalloc(&c->d.csr_vin, pm));
     KP_TRY(dalloc(&c->d.csr_keys, pm));
     KP_TRY(dalloc(&c->d.csr_vals, pm));
-    KP_TRY(dalloc(&c->d.pass_flag, 64));
+    KP_TRY(dalloc(&c->d.pass_flag, kPassFlagWords));
+    KP_TRY(dalloc(&c->d.sdone, u));
     KP_TRY(dalloc(&c->d.counters, 64));
     KP_TRY(dalloc(&c->d.stats, 1));
     c->d.temp_bytes = rocprim_temp_bytes((int32_t)std::min<size_t>(pm, INT32_MAX));
@@ -334,6 +335,9 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = knob("KP_COMPACT_MAX")) c->compact_max = std::atoi(e);
   if (const char *e = knob("KP_FUSED")) c->fused_enabled = std::atoi(e) != 0;
   if (const char *e = knob("KP_ACC_LIST")) c->acc_list = std::atoi(e);
+  if (const char *e = knob("KP_PASS_LOOP")) c->pass_loop_enabled = std::atoi(e) != 0;
+  if (const char *e = knob("KP_PASS_LOOP_FORM")) c->pass_loop_form = std::atoi(e) == 1 ? 1 : 2;
+  if (const char *e = knob("KP_PASS_LOOP_PMAX")) c->pass_loop_pmax = std::max(1, std::min(256, std::atoi(e)));
   if (const char *e = knob("KP_KEYS_MERGE")) c->keys_merge_enabled = std::atoi(e) != 0;
   if (const char *e = knob("KP_ROUND_BEGIN")) c->round_begin = std::atoi(e) != 0;
   if (const char *e = knob("KP_CSR_SORT")) c->csr_count_enabled = std::atoi(e) == 0;
@@ -752,6 +756,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
       if (!ptr) return fail(KP_ENOMEM, "kp_solve: a device buffer is missing");
   }
   KP_TRY(launch_reset_units(c, p->tie_seed));  // also the salts of the rotated tie-break
+  loop_profile_reset();  // KP_LOOP_PROFILE builds only
   c->pack_sp = sp;
   c->pack_canonical = true;  // the solve scores in canonical column order
   const int32_t shard = c->u_hi - c->u_lo;
@@ -796,7 +801,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   KP_TRY(E.make(&t0, hipEventDefault));
   KP_TRY(E.make(&t1, hipEventDefault));
   KP_HIP(hipMemsetAsync(c->d.stats, 0, sizeof(SolveStats), c->stream));
-  KP_HIP(hipMemsetAsync(c->d.pass_flag, 0, sizeof(int32_t) * 64, c->stream));
+  KP_HIP(hipMemsetAsync(c->d.pass_flag, 0, sizeof(int32_t) * kPassFlagWords, c->stream));
   KP_HIP(hipEventRecord(t0, c->stream));
   std::vector<int32_t> round_active;  // exact active units per round (when known)
   kp_timing tm{};
@@ -845,6 +850,13 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   auto passes_of_round = [&](int32_t A, const int32_t *A_dev) -> int {
     // also opens the slots, banks + clears the pass flags
     KP_TRY(launch_csr_build(c, A, K, A_dev));
+    // small rounds: every pass in one persistent launch
+    bool looped = false;
+    KP_TRY(launch_pass_loop(c, sp, A, A_dev, p->max_passes, &looped));
+    if (looped) {
+      tm.loop_rounds++;
+      return KP_OK;
+    }
     // passes run back to back on the device: no host round trip inside a round
     for (int32_t pass = 0; pass < p->max_passes; ++pass) {
       KP_TRY(launch_plan(c, sp, A, pass, A_dev));
@@ -989,6 +1001,10 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
                           c->stream));
   SolveStats dst{};
   KP_HIP(hipMemcpyAsync(&dst, c->d.stats, sizeof dst, hipMemcpyDeviceToHost, c->stream));
+  int32_t *loop_err = c->pinned + 384;
+  *loop_err = 0;
+  KP_HIP(hipMemcpyAsync(loop_err, c->d.pass_flag + kLoopErr, sizeof(int32_t), hipMemcpyDeviceToHost,
+                        c->stream));
   if (c->world > 1) {
     hipEvent_t evF;
     KP_TRY(E.make(&evF, hipEventDisableTiming));
@@ -997,6 +1013,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     KP_HIP(hipStreamSynchronize(c->stream));
   }
   c->in_collective = false;  // every collective of this solve completed
+  if (*loop_err) return fail(KP_EHIP, "kp_solve: a pass-loop grid barrier timed out");
   const int32_t rounds = (int32_t)dst.rounds, passes = (int32_t)dst.passes;
   const int64_t pairs = dst.active_sum * N;
   tm.solve_ms = ev_ms(t0, t1);
@@ -1168,6 +1185,7 @@ void kp_destroy(kp_ctx *c) {
   }
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  loop_profile_dump();  // KP_LOOP_PROFILE builds only: the last solve's pass-loop phases
   if (c->nccl_comm) ncclCommDestroy(static_cast<ncclComm_t>(c->nccl_comm));
   DevState &d = c->d;
   if (d.fz_prof) {  // KP_FZ_PROF: the accumulated phase clocks
@@ -1208,7 +1226,7 @@ void kp_destroy(kp_ctx *c) {
                   d.inv, d.ent_unit,
                   d.ent_slot, d.ent_size, d.ent_lead, d.ent_q, d.perm,
                   d.csr_kin, d.csr_vin,
-                  d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
+                  d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.sdone, d.counters,
                   d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.roff,
                   d.rreq, d.rsuf, d.rprio, d.pre_node, d.pre_vict, d.pre_cost,
                   d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.nrec, d.nst, d.stats, d.np32, d.colnode, d.wshift, d.part, d.fz_prof,

@@ -28,6 +28,12 @@ static_assert(kTieMul * kTieMulInv == 1u, "tie multiplier must be invertible");
 
 enum UnitStatus : int32_t { kActive = 0, kPlaced = 1, kNoFit = 2 };
 
+// d.pass_flag layout: [0, 64) productive-pass flags of the current round,
+// [kLoopBar] the persistent pass loop's barrier counter (zeroed at every round
+// start), [kLoopErr] its timeout flag (zeroed at every solve start)
+constexpr int kPassFlagWords = 128;
+constexpr int kLoopBar = 64, kLoopErr = 65;
+
 // Solve statistics accumulated on the device (no per-round host round trip):
 // rounds with active units, sum of active units over rounds (x N = pairs
 // scored) and productive passes.
@@ -118,7 +124,8 @@ struct DevState {
   int32_t *node_list = nullptr; // [N] nodes with bidders this round (count: counters[32])
   int4 *nrec = nullptr;
   uint32_t *nst = nullptr;      // [N][16] static plan record (D <= 4, fits32): cap, R, K per dim, base, topo         // [N] per node_list entry {node, seg_start, seg_end, 0} (plan pass 0)
-  int32_t *pass_flag = nullptr; // [64] pass p produced proposals
+  int32_t *pass_flag = nullptr; // [kPassFlagWords] pass p produced proposals (+ pass loop words)
+  int32_t *sdone = nullptr;     // [U] k_pass_loop: slot closed (placed / no plan) this round
   // preemption: unit priorities, victim-pool CSR sorted
   // (node, prio desc, running index asc) with per-node suffix sums, outputs
   int32_t *uprio = nullptr;     // [U]
@@ -192,6 +199,14 @@ struct kp_ctx {
   // one per node); 2,048: config #5 batches -2 %, config #3 neutral (tools/ab_*env.sh)
   int32_t acc_waves = 2048;
   int32_t acc_list = 1;  // KP_ACC_LIST=0: k_accept walks every node while entries >= nodes
+  // persistent pass loop (k_pass_loop / k_pass_loop2): rounds whose slots fit
+  // P <= pass_loop_pmax workgroups run all their passes in one launch. A
+  // measured alternative, off by default (KP_PASS_LOOP=1 turns it on;
+  // KP_PASS_LOOP_PMAX: largest grid): bit-identical, but a pass costs about
+  // what its two launches cost (profiles/r03_pass_loop_*)
+  bool pass_loop_enabled = false;
+  int32_t pass_loop_pmax = 64;
+  int32_t pass_loop_form = 2;  // KP_PASS_LOOP_FORM: 2 register-resident (k_pass_loop2), 1 reloading
   // KP_COMPACT_MAX: largest unit range compacted by the one-workgroup kernel
   int32_t compact_max = 262144;
   bool round_begin = true;  // KP_ROUND_BEGIN=0: round start + compaction as two launches
@@ -291,6 +306,12 @@ int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass,
 int launch_active_async(kp_ctx *c, int32_t lo, int32_t hi, int32_t *count_host,
                         bool *direct = nullptr);
 int launch_accept(kp_ctx *c, const ScoreParams &sp, int32_t pass, int32_t A);
+// KP_LOOP_PROFILE builds: per-pass phase stamps of k_pass_loop (stderr)
+void loop_profile_dump();
+void loop_profile_reset();
+// every pass of the round in one persistent launch (*done), if the round qualifies
+int launch_pass_loop(kp_ctx *c, const ScoreParams &sp, int32_t A, const int32_t *A_dev,
+                     int32_t max_passes, bool *done);
 // the static per-node plan records d.nst (every solve, after the division tables)
 int launch_node_rec(kp_ctx *c);
 void launch_probe(kp_ctx *c, const ScoreParams &sp, int32_t A);

@@ -545,6 +545,7 @@ __device__ __forceinline__ void round_keys_init(const RoundKeys &rk, int64_t t) 
     if (rk.pass_flag[t] != 0)
       atomicAdd(reinterpret_cast<unsigned long long *>(&rk.st->passes), 1ull);
     rk.pass_flag[t] = 0;
+    if (t == 0) rk.pass_flag[kLoopBar] = 0;  // the pass loop's barrier counter
   }
 }
 

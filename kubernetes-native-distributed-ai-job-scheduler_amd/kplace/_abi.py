@@ -94,7 +94,7 @@ class Timing(C.Structure):
         ("solve_ms", C.c_double), ("score_ms", C.c_double),
         ("select_ms", C.c_double), ("accept_ms", C.c_double),
         ("score_launches", C.c_int64), ("score_bytes", C.c_int64),
-        ("select_bytes", C.c_int64), ("fused", C.c_int32), ("reserved", C.c_int32),
+        ("select_bytes", C.c_int64), ("fused", C.c_int32), ("loop_rounds", C.c_int32),
     ]
 
 

@@ -133,38 +133,50 @@ def config3(J: int = 100_000, N: int = 10_000) -> Workload:
 
 
 def prefill_running(seed: int, cap: np.ndarray, occupancy: float, probes: int = 64):
-    """Pre-place synthetic running jobs (the victim pool of config #4).
+    """Pre-place synthetic running jobs (the victim pool of config #4) until
+    Sum(used)/Sum(cap) >= `occupancy` in EVERY dim.
 
     Running job k draws its request and priority like a pending job (seed +
     0x1000, so the draws are independent of the queue) and a start node
     x mod N (stream 2); it goes to the first node of start, start+1, ...
-    (at most `probes`) where it fits, or is dropped. Jobs are added until the
-    GPU-count dimension reaches `occupancy` of its capacity (SURVEY §8d asks
-    >= 30% per dim; with this job mix GPUs saturate long before memory reaches
-    30%: a job takes ~28% of a mean node's GPUs but ~6% of its memory, so the
-    per-dim rule is unreachable and the scarce GPU dimension sets the level).
+    (at most `probes`) where it fits, or is dropped. Phase 1 places the draws
+    as drawn until both GPU dims (count, memory) reach `occupancy`; GPU memory
+    is the later one (a job asks 16-288 GiB per GPU of a node's 288), so the
+    GPU count ends near 0.53 at occupancy 0.30. Phase 2 continues the same
+    stream with the GPU fields of each draw zeroed (GPU-less jobs, e.g. the
+    CPU side of a serving stack) until CPU and memory reach `occupancy` too.
     Returns (used [D, N], node [R], req [D, R], prio [R])."""
     D_, N = cap.shape
     used = np.zeros_like(cap)
-    target = occupancy * cap[2].sum()
+    tot = cap.sum(1).astype(np.float64)
+    sums = np.zeros(D_, np.float64)
     rs = seed + 0x1000
     nodes, reqs, prios = [], [], []
+    gpu_dims = [d for d in (2, 3) if d < D_]
+    phase = 1
     k = 0
     batch = 4096
-    while used[2].sum() < target and k < 20 * N:
+    done = False
+    while not done and k < 40 * N:
         _, rq, pr = make_crs(rs, k + batch, gangs=False)
         starts = (splitmix64(rs, 2, np.arange(k, k + batch, dtype=np.uint64))
                   % np.uint64(N)).astype(np.int64)
         for i in range(batch):
-            if used[2].sum() >= target:
+            if phase == 1 and all(sums[d] >= occupancy * tot[d] for d in gpu_dims):
+                phase = 2
+            if phase == 2 and bool(np.all(sums >= occupancy * tot)):
+                done = True
                 break
-            q = rq[:, k + i]
+            q = rq[:, k + i].copy()
+            if phase == 2:
+                q[gpu_dims] = 0
             cand = (starts[i] + np.arange(probes)) % N
             fits = np.all(used[:, cand] + q[:, None] <= cap[:, cand], axis=0)
             hit = np.flatnonzero(fits)
             if hit.size:
                 n = int(cand[hit[0]])
                 used[:, n] += q
+                sums += q
                 nodes.append(n)
                 reqs.append(q)
                 prios.append(int(pr[k + i]))
@@ -176,7 +188,8 @@ def prefill_running(seed: int, cap: np.ndarray, occupancy: float, probes: int = 
 def config4(J: int = 200_000, N: int = 20_000, occupancy: float = 0.30) -> Workload:
     """#4: priority tiers 0-3 against a cluster pre-filled with running jobs
     (priorities 0-3; the victim pool for preemption scoring, w.meta['run_*'])
-    up to `occupancy` of its GPUs. Singletons (one pod each), shapes A-D."""
+    until every dim is at least `occupancy` used (prefill_running). Singletons
+    (one pod each), shapes A-D."""
     seed = SEED_BASE + 4
     cap, topo = make_nodes(seed, N, ab_only=False)
     size, req_cr, prio_cr = make_crs(seed, J, gangs=False)

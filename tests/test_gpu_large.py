@@ -37,7 +37,7 @@ def test_config4_full_size_parity_and_properties():
                run_req=m["run_req"], run_prio=m["run_prio"])
     assert {k: digest(v) for k, v in ins.items()} == g4["inputs"], "config #4 generator changed"
     util = w.used.sum(1) / w.cap.sum(1)
-    assert util[2] >= 0.30
+    assert (util >= 0.30).all(), util  # >= 0.30 in every dim
     p = _abi.default_params(**synth.CONFIG_PARAMS[4])
     with Placer(device=0) as pl:
         pl.load_nodes(w.cap, w.used, w.topo)

@@ -269,6 +269,44 @@ def test_csr_build_paths_parity(oracle, monkeypatch, knobs):
     _assert_same(g2, o, f"csr {knobs} second solve")
 
 
+@pytest.mark.parametrize("form", ["1", "2"])
+@pytest.mark.parametrize("pmax,cfg", [("64", (3, 20_000, 2_000)), ("256", (3, 20_000, 2_000)),
+                                      ("8", (2, 6_000, 600)), ("64", (4, 8_000, 1_500))])
+def test_pass_loop_parity(oracle, monkeypatch, form, pmax, cfg):
+    """The persistent pass loop (KP_PASS_LOOP=1, a measured alternative that
+    is off by default): every pass of a qualifying round in one launch of
+    resident workgroups with grid barriers; form 1 reloads the pass state,
+    form 2 keeps each wave's slot group and bid node in registers. Same
+    placement, rounds and passes as the oracle."""
+    monkeypatch.setenv("KP_PASS_LOOP", "1")
+    monkeypatch.setenv("KP_PASS_LOOP_FORM", form)
+    monkeypatch.setenv("KP_PASS_LOOP_PMAX", pmax)
+    no, J, N = cfg
+    w = synth.config(no, J, N)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[no])
+    with Placer(device=0) as pl:
+        g = pl.place(w, p)
+        looped = pl.timing()["loop_rounds"]
+        g2 = pl.place(w, p)
+    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
+    assert looped > 0, "no round took the pass loop"
+    _assert_same(g, o, f"pass loop form {form} pmax {pmax}")
+    _assert_same(g2, o, f"pass loop form {form} pmax {pmax}, second solve")
+
+
+def test_pass_loop_random_parity(oracle, monkeypatch):
+    """The pass loop on random snapshots with gangs, both score modes, D <= 4
+    (the loop's instantiations) and 32-candidate lists."""
+    monkeypatch.setenv("KP_PASS_LOOP", "1")
+    for seed, D, K, mode in ((3, 4, 16, 0), (4, 3, 32, 1), (5, 2, 8, 0), (6, 1, 16, 1)):
+        w = random_workload(500 + seed, J=3_000, N=400, D=D)
+        p = _abi.default_params(n_cand=K, score_mode=mode, gpu_dim=min(2, D - 1))
+        with Placer(device=0) as pl:
+            g = pl.place(w, p)
+        o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
+        _assert_same(g, o, f"pass loop random seed {seed}")
+
+
 def test_csr_scan_many_nodes(oracle):
     """More than one 65,536-node tile in the node scan of the counting-mode
     bidder index (running carry between tiles)."""
@@ -578,8 +616,8 @@ def test_preempt_random_parity(oracle, placer, seed):
 
 
 def test_preempt_config4_parity(oracle, placer):
-    """BASELINE config #4 shape at 1/10 size: priority tiers, 30% GPU
-    occupancy of running jobs, preemption candidates for every NO_FIT job."""
+    """BASELINE config #4 shape at 1/10 size: priority tiers, running jobs
+    filling every dim to >= 30%, preemption candidates for every NO_FIT job."""
     w = synth.config4(20_000, 2_000)
     p = _abi.default_params(**synth.CONFIG_PARAMS[4])
     m = w.meta

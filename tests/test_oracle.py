@@ -323,7 +323,7 @@ def test_preempt_matches_python_spec(oracle, seed):
 def test_config4_generator_occupancy():
     w = synth.config4(4000, 400)
     util = w.used.sum(1) / w.cap.sum(1)
-    assert util[2] >= 0.30
+    assert (util >= 0.30).all(), util  # Sum(used)/Sum(cap) >= 0.30 per dim
     rn, rq, rp = w.meta["run_node"], w.meta["run_req"], w.meta["run_prio"]
     back = np.zeros_like(w.used)
     np.add.at(back.T, rn, rq.T)
