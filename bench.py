@@ -300,11 +300,11 @@ def main():
     ap.add_argument("--c4-nodes", type=int, default=20_000)
     ap.add_argument("--c4-steps", type=int, default=3)
     ap.add_argument("--no-config4", action="store_true")
-    ap.add_argument("--cpu-c4-jobs", type=int, default=10_000,
+    ap.add_argument("--cpu-c4-jobs", type=int, default=25_000,
                     help="config #4 CPU baseline sample: the first N pending jobs")
-    ap.add_argument("--cpu-c4-rounds", type=int, default=2,
+    ap.add_argument("--cpu-c4-rounds", type=int, default=3,
                     help="config #4 CPU baseline sample: rounds of their solve")
-    ap.add_argument("--cpu-stream-batches", type=int, default=2,
+    ap.add_argument("--cpu-stream-batches", type=int, default=4,
                     help="config #5 CPU baseline sample: the first N micro-batches")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="time the steps without per-launch HIP events (no roofline)")
