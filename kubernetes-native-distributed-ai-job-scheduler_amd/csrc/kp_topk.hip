@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "kp_device.hpp"
 #include "kp_internal.hpp"
@@ -347,26 +348,57 @@ void k_score_topk(
         cur.load(srec[wave][i]);
         const uint32_t wq = cur[2 * D + 2], qg = cur[D], af = cur[D + 1];
         const int32_t wfr = (int32_t)cur[2 * D + 3];
-        int32_t sv[2];
+        // the row's terms, wave-uniform: a request no column of the wave's
+        // class can meet scores nothing; the GPU-fit bonus only exists for a
+        // GPU request (wfr != 0) and the affinity bonus for an affinity
+        // domain (af >= 0), so rows without them skip those compares
+        // dims past DL whose request is 0 are skipped: they always fit
+        // (free >= 0) and add no carry (q = 0: threshold c > every a); dim 0
+        // is always tested (padding columns fail it)
+        auto score = [&](auto hasg, auto hasa, auto dl) {
+          constexpr int DL = decltype(dl)::value;
+          int32_t sv[2];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          // fit: every free - q >= 0; operands < 2^30, so the signed
-          // differences are exact and one min replaces D compares
-          int32_t mn = (int32_t)(f_[k][0] - cur[0]);
+          for (int k = 0; k < 2; ++k) {
+            // fit: every free - q >= 0; operands < 2^30, so the signed
+            // differences are exact and one min replaces D compares
+            int32_t mn = (int32_t)(f_[k][0] - cur[0]);
 #pragma unroll
-          for (int d = 1; d < D; ++d) mn = min(mn, (int32_t)(f_[k][d] - cur[d]));
-          int32_t acc = wa_[k] + (int32_t)wq + 1;  // s + 1
+            for (int d = 1; d < DL; ++d) mn = min(mn, (int32_t)(f_[k][d] - cur[d]));
+            int32_t acc = wa_[k] + (int32_t)wq + 1;  // s + 1
 #pragma unroll
-          for (int d = 0; d < D; ++d) acc += a_[k][d] >= cur[D + 2 + d] ? wv[d] : 0;
-          // GPU-topology fit and the CacheStrategy=shared affinity bonus
-          const int32_t bonus = (fg_[k] == qg ? wfr : 0) + (tp_[k] == af ? waffv : 0);
-          const int32_t sc = (MOST ? acc : b_[k] + 2 - acc) + bonus;
-          sv[k] = mn >= 0 ? sc : 0;  // s + 1, 0 = infeasible
-        }
+            for (int d = 0; d < DL; ++d) acc += a_[k][d] >= cur[D + 2 + d] ? wv[d] : 0;
+            // GPU-topology fit and the CacheStrategy=shared affinity bonus
+            int32_t bonus = 0;
+            if constexpr (decltype(hasg)::value) bonus += fg_[k] == qg ? wfr : 0;
+            if constexpr (decltype(hasa)::value) bonus += tp_[k] == af ? waffv : 0;
+            const int32_t sc = (MOST ? acc : b_[k] + 2 - acc) + bonus;
+            sv[k] = mn >= 0 ? sc : 0;  // s + 1, 0 = infeasible
+          }
           if constexpr (H16)
-          ssc[buf][i][wave * 64 + lane] = (uint32_t)sv[0] | ((uint32_t)sv[1] << 16);
-        else
-          reinterpret_cast<int2 *>(ssc[0][i])[wave * 64 + lane] = make_int2(sv[0], sv[1]);
+            ssc[buf][i][wave * 64 + lane] = (uint32_t)sv[0] | ((uint32_t)sv[1] << 16);
+          else
+            reinterpret_cast<int2 *>(ssc[0][i])[wave * 64 + lane] = make_int2(sv[0], sv[1]);
+        };
+        using T_ = std::true_type;
+        using F_ = std::false_type;
+        using DA = std::integral_constant<int, D>;
+        using D2 = std::integral_constant<int, 2>;  // D = 4: no GPU request in dims 2, 3
+        const bool hasg = wfr != 0, hasa = (int32_t)af >= 0;
+        bool hi0 = false;
+        if constexpr (D == 4) hi0 = (cur[2] | cur[3]) == 0u;
+        if (cur[0] == 0x7FFFFFFFu) {  // no column of this class fits the row
+          if constexpr (H16)
+            ssc[buf][i][wave * 64 + lane] = 0u;
+          else
+            reinterpret_cast<int2 *>(ssc[0][i])[wave * 64 + lane] = make_int2(0, 0);
+        } else if (hasg) {  // a GPU-fit bonus implies a GPU request: all dims
+          if (hasa) score(T_{}, T_{}, DA{}); else score(T_{}, F_{}, DA{});
+        } else if (hi0) {
+          if (hasa) score(F_{}, T_{}, D2{}); else score(F_{}, F_{}, D2{});
+        } else {
+          if (hasa) score(F_{}, T_{}, DA{}); else score(F_{}, F_{}, DA{});
+        }
       }
     }
     KP_FZ_PROF_MARK(3);
