@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 4  /* 4: kp_last_error_r */
+#define KP_ABI_VERSION 5  /* 4: kp_last_error_r; 5: kp_timing.incr_rounds */
 
 /* ---- limits ------------------------------------------------------------ */
 #define KP_MAX_DIMS 8       /* resource dimensions per job/node               */
@@ -272,6 +272,9 @@ typedef struct kp_timing {
   int32_t fused;            /* 1: fused filter+score+top-K (no score matrix;
                                score_* then time/count k_score_topk)         */
   int32_t loop_rounds;      /* rounds whose passes ran as one persistent launch */
+  int32_t incr_rounds;      /* rounds whose candidates came from the incremental
+                               update (score_* then cover the full scans only) */
+  int32_t pad;
 } kp_timing;
 int kp_last_timing(kp_ctx *ctx, kp_timing *t);
 

@@ -131,7 +131,29 @@ static int ensure_nodes(kp_ctx *c, int32_t N, int32_t D) {
   KP_TRY(dalloc(&c->d.nrec, (size_t)n + 16));
   KP_TRY(dalloc(&c->d.nst, (size_t)n * 16));
   KP_TRY(dalloc(&c->d.perm, (size_t)n));
+  KP_TRY(dalloc(&c->d.npos, (size_t)n));
+  KP_TRY(dalloc(&c->d.clist, (size_t)2 * n));
+  KP_TRY(dalloc(&c->d.chg, (size_t)n));
+  // usage-change stamps: round serials start at 0
+  KP_HIP(hipMemsetAsync(c->d.chg, 0xFF, sizeof(int32_t) * (size_t)n, c->stream));
   c->cap_N = n;
+  return KP_OK;
+}
+
+// per-unit lists of the incremental candidate phase (kp_incr.hip) and the
+// per-round rescan rows
+static int ensure_incr(kp_ctx *c, int32_t U, int32_t KL) {
+  if (c->d.ukey && U <= c->cap_incr_U && KL <= c->cap_incr_KL) return KP_OK;
+  c->cap_incr_U = 0;
+  const size_t u = (size_t)std::max(U, 64);
+  KP_TRY(dalloc(&c->d.ukey, u * KL));
+  KP_TRY(dalloc(&c->d.unode, u * KL));
+  KP_TRY(dalloc(&c->d.ucnt, u));
+  KP_TRY(dalloc(&c->d.ubound, u));
+  KP_TRY(dalloc(&c->d.rs_slot, u));
+  KP_TRY(dalloc(&c->d.rs_unit, u));
+  c->cap_incr_U = (int32_t)u;
+  c->cap_incr_KL = KL;
   return KP_OK;
 }
 
@@ -334,6 +356,9 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = knob("KP_SCORE_NPL")) c->score_npl = std::atoi(e) == 4 ? 4 : 2;
   if (const char *e = knob("KP_COMPACT_MAX")) c->compact_max = std::atoi(e);
   if (const char *e = knob("KP_FUSED")) c->fused_enabled = std::atoi(e) != 0;
+  if (const char *e = knob("KP_INCR")) c->incr_enabled = std::atoi(e) != 0;
+  if (const char *e = knob("KP_INCR_CTHR_DIV")) c->incr_cthr_div = std::max(1, std::atoi(e));
+  if (const char *e = knob("KP_INCR_TRACE")) c->incr_trace = std::atoi(e) != 0;
   if (const char *e = knob("KP_ACC_LIST")) c->acc_list = std::atoi(e);
   if (const char *e = knob("KP_PASS_LOOP")) c->pass_loop_enabled = std::atoi(e) != 0;
   if (const char *e = knob("KP_PASS_LOOP_FORM")) c->pass_loop_form = std::atoi(e) == 1 ? 1 : 2;
@@ -487,6 +512,16 @@ static int load_nodes_impl(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap,
                           hipMemcpyHostToDevice, c->stream));
     KP_HIP(hipMemcpyAsync(c->d.perm, c->h_perm.data(), sizeof(int32_t) * N,
                           hipMemcpyHostToDevice, c->stream));
+    std::vector<int32_t> npos;
+    try {
+      npos.resize(N);
+    } catch (const std::bad_alloc &) {
+      return fail(KP_ENOMEM, "kp_load_nodes: host copy");
+    }
+    for (int32_t i = 0; i < N; ++i) npos[(size_t)c->h_perm[i]] = i;
+    KP_HIP(hipMemcpyAsync(c->d.npos, npos.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice,
+                          c->stream));
+    KP_HIP(hipStreamSynchronize(c->stream));  // npos is a local
   }
   // the victim pool belongs to the previous node table
   KP_HIP(hipMemsetAsync(c->d.roff, 0, sizeof(int32_t) * ((size_t)N + 1), c->stream));
@@ -778,12 +813,32 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   c->pack_fused = fused;
   c->pack_full = true;
   c->last_fused = fused;
+  // Incremental candidate phase (kp_incr.hip): the first round scans in full
+  // and keeps every unit's top-KL list (KL >= K, the merge holds <= 2,048
+  // keys per row); later rounds re-score only the nodes the previous round
+  // changed. Needs the one-launch round start (it compacts the changed nodes).
+  const int32_t ntiles = std::max(c->fz_P / 1024, 1);
+  const bool incr = fused && c->incr_enabled && c->round_begin && shard > 0 &&
+                    shard <= c->compact_max;
+  const int32_t KL = incr ? std::min<int32_t>(KP_MAX_CAND, std::max<int32_t>(K, 2048 / ntiles)) : K;
+  c->incr_active = incr;
+  struct IncrOff {  // the flag never outlives the solve (the accept kernels read it)
+    kp_ctx *c;
+    ~IncrOff() { c->incr_active = false; }
+  } incr_off{c};
+  ScoreParams sp_list = sp;
+  sp_list.n_cand = KL;
   int64_t rpc = rows_per_chunk(c);
   if (fused) {
     rpc = INT64_MAX;  // no matrix, no chunks: per row only tiles x K keys
-    KP_TRY(ensure_part(c, (int64_t)std::max(shard, 1) * (c->fz_P / 1024) * K));
+    KP_TRY(ensure_part(c, (int64_t)std::max(shard, 1) * (c->fz_P / 1024) * KL));
     if (!c->d.part || !c->d.colnode || !c->d.wshift)
       return fail(KP_ENOMEM, "kp_solve: a fused-path buffer is missing");
+    if (incr) {
+      KP_TRY(ensure_incr(c, U, KL));
+      if (!c->d.ukey || !c->d.chg || !c->d.clist || !c->d.npos)
+        return fail(KP_ENOMEM, "kp_solve: an incremental-phase buffer is missing");
+    }
   } else {
     KP_TRY(ensure_matrix(c, (int32_t)std::min<int64_t>(std::max(shard, 1), rpc)));
   }
@@ -802,13 +857,33 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   KP_TRY(E.make(&t1, hipEventDefault));
   KP_HIP(hipMemsetAsync(c->d.stats, 0, sizeof(SolveStats), c->stream));
   KP_HIP(hipMemsetAsync(c->d.pass_flag, 0, sizeof(int32_t) * kPassFlagWords, c->stream));
+  // changed-node and rescan counters of both round parities
+  KP_HIP(hipMemsetAsync(c->d.counters + kCCount, 0, sizeof(int32_t) * 4, c->stream));
   KP_HIP(hipEventRecord(t0, c->stream));
   std::vector<int32_t> round_active;  // exact active units per round (when known)
   kp_timing tm{};
   // filter+score and top-K select of `rows` rows starting at act_local[r0];
   // rows_dev (nullable) clamps them to the device count
+  const ListOut lo_none{nullptr, nullptr, nullptr, nullptr, nullptr, K};
+  const ListOut lo_full{c->d.ukey, c->d.unode, c->d.ucnt, c->d.ubound, nullptr, K};
+  const ListOut lo_rescan{c->d.ukey, c->d.unode, c->d.ucnt, c->d.ubound, c->d.rs_slot, K};
   auto score_select = [&](int64_t r0, int32_t rows, const int32_t *rows_dev,
                           int32_t round) -> int {
+    if (incr && round > 0) {
+      // incremental round: the lists absorb the changed nodes; the rows they
+      // cannot answer are rescanned (k_score_topk + merge over the round's
+      // rescan list, device count; not bracketed by the profiling events)
+      c->keys_in_merge = false;
+      if (c->world == 1 && c->keys_merge_enabled && rows > 0) {
+        KP_TRY(csr_prepare(c, rows, K));
+        c->keys_in_merge = c->csr_mode == 1;
+      }
+      KP_TRY(launch_cand_update(c, sp, KL, rows, rows_dev, round, c->keys_in_merge));
+      KP_TRY(launch_score_topk(c, sp_list, c->d.rs_unit, rows, ksh, c->d.cand_local,
+                               c->d.counters + kRsCount + (round & 1), lo_rescan, false));
+      tm.incr_rounds++;
+      return KP_OK;
+    }
     // profiling brackets the filter+score launch only (each event record is
     // a GPU packet of a few us: the select is timed by rocprofv3 instead)
     KEv ke{nullptr, nullptr, round, rows};
@@ -829,8 +904,9 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
       }
       // the profiling bracket ends right after k_score_topk (before the merge)
       c->fz_end_event = c->profiling ? ke.b : nullptr;
-      const int rc = launch_score_topk(c, sp, c->d.act_local + r0, rows, ksh,
-                                       c->d.cand_local + r0 * K, rows_dev);
+      const int rc = launch_score_topk(c, incr ? sp_list : sp, c->d.act_local + r0, rows, ksh,
+                                       c->d.cand_local + r0 * K, rows_dev,
+                                       incr ? lo_full : lo_none, true);
       c->fz_end_event = nullptr;
       KP_TRY(rc);
     } else {
@@ -909,6 +985,8 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     };
     for (int32_t r = 0; A_bound > 0; ++r) {
       if (p->max_rounds > 0 && r >= p->max_rounds) break;
+      c->incr_round = r;
+      c->cur_serial = c->round_serial++;
       bool direct = true;
       KP_TRY(launch_active_async(c, c->u_lo, c->u_hi, A_h, &direct));
       if (!direct) KP_HIP(hipEventRecord(evA, c->stream));
@@ -926,6 +1004,16 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
       const int32_t *A_dev = c->d.counters;
       KP_TRY(score_select(0, (int32_t)A_bound, A_dev, r));
       KP_TRY(passes_of_round((int32_t)A_bound, A_dev));
+      if (c->incr_trace && incr) {  // diagnostics: synchronous per-round counters
+        int32_t h[4] = {0, 0, 0, 0};
+        KP_HIP(hipMemcpyAsync(h, c->d.counters, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+        KP_HIP(hipMemcpyAsync(h + 1, c->d.counters + kCCount + (r & 1), sizeof(int32_t),
+                              hipMemcpyDeviceToHost, c->stream));
+        KP_HIP(hipMemcpyAsync(h + 2, c->d.counters + kRsCount + (r & 1), sizeof(int32_t),
+                              hipMemcpyDeviceToHost, c->stream));
+        KP_HIP(hipStreamSynchronize(c->stream));
+        std::fprintf(stderr, "kp_incr round %d active %d changed %d rescanned %d\n", r, h[0], h[1], h[2]);
+      }
       KP_TRY(round_count(direct));  // landed long ago on a busy round
       round_active.push_back(*A_h);
       A_bound = *A_h;
@@ -958,6 +1046,8 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     int64_t G_bound = U;
     for (int32_t r = 0; G_bound > 0; ++r) {
       if (p->max_rounds > 0 && r >= p->max_rounds) break;
+      c->incr_round = r;
+      c->cur_serial = c->round_serial++;
       const int32_t B = (int32_t)std::min<int64_t>(Smax, G_bound);  // per-rank slot bound
       if (shard > 0) {
         KP_TRY(launch_active_async(c, c->u_lo, c->u_hi, Al_h));

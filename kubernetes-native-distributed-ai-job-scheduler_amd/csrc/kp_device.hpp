@@ -446,6 +446,53 @@ __device__ __forceinline__ int32_t key_node(uint64_t key, uint32_t sl, uint32_t 
 }
 inline int blocks(int64_t n, int b) { return (int)((n + b - 1) / b); }
 
+// rank of this lane among the set lanes of m below it (ballot compaction)
+__device__ __forceinline__ int mbcnt64(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// k_csr_keys' per-round state reset, thread t of the extra workgroups of the
+// kernel that opens the round's slots (the candidate merge or the incremental
+// candidate update, rk.enabled): round statistics, the previous round's
+// productive passes, node segments / flags, window flags
+__device__ __forceinline__ void round_keys_init(const RoundKeys &rk, int64_t t) {
+  if (t == 0) {
+    const int32_t Aa = rk.A_dev ? min(rk.A, *rk.A_dev) : rk.A;
+    if (Aa > 0) {
+      rk.st->rounds += 1;
+      rk.st->active_sum += Aa;
+    }
+    *rk.nl_count = 0;
+  }
+  if (t < rk.N) {
+    rk.seg_start[t] = -1;
+    rk.node_flag[t] = -1;
+  }
+  if (t < rk.nwin) rk.win[t] = -1;
+  if (t < 64) {
+    if (rk.pass_flag[t] != 0)
+      atomicAdd(reinterpret_cast<unsigned long long *>(&rk.st->passes), 1ull);
+    rk.pass_flag[t] = 0;
+    if (t == 0) rk.pass_flag[kLoopBar] = 0;  // the pass loop's barrier counter
+  }
+}
+
+// k_csr_keys' per-slot work for slot `slot` of unit `unit` whose candidate
+// list (lane < K: node, -1 = none) is final: bids cleared, the slot's bitmap
+// bit set in the row of every candidate node, the slot opened (or NO_FIT)
+__device__ __forceinline__ void round_keys_slot(const RoundKeys &rk, int32_t slot, int32_t unit,
+                                                int32_t K, int32_t node, int lane) {
+  if (lane < K) {
+    rk.bid[(int64_t)slot * K + lane] = 0xFFFFFFFFu;  // kNoBid
+    if (node >= 0) atomicOr(&rk.bm[(int64_t)node * rk.Wb + (slot >> 5)], 1u << (slot & 31));
+  }
+  const int32_t first = __shfl(node, 0, 64);
+  if (lane == 0) {
+    rk.open[slot] = first >= 0 ? 1 : 0;
+    if (first < 0) rk.status[unit] = kNoFit;
+  }
+}
+
 template <template <int> class F, typename... Args>
 int dispatch_D(int D, Args &&...args) {
   switch (D) {

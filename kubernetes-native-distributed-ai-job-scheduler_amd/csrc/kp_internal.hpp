@@ -33,6 +33,11 @@ enum UnitStatus : int32_t { kActive = 0, kPlaced = 1, kNoFit = 2 };
 // start), [kLoopErr] its timeout flag (zeroed at every solve start)
 constexpr int kPassFlagWords = 128;
 constexpr int kLoopBar = 64, kLoopErr = 65;
+// d.counters words: [0] this rank's active units, [1] the global count, [32]
+// bid nodes of the round, [33] bidder entries, [kCCount + r % 2] nodes changed
+// before round r, [kRsCount + r % 2] rows rescanned in round r (incremental
+// candidate phase), [40, 56) launch probes
+constexpr int kCCount = 36, kRsCount = 38;
 
 // Solve statistics accumulated on the device (no per-round host round trip):
 // rounds with active units, sum of active units over rounds (x N = pairs
@@ -53,6 +58,19 @@ struct RoundKeys {
   uint8_t *open;
   const int32_t *A_dev;
   struct SolveStats *st;
+};
+
+// Per-unit candidate lists of the incremental candidate phase (kp_incr.hip):
+// the merge of a full scan writes them (ukey != nullptr) with kout = the
+// solve's n_cand candidates per slot; rslot (nullable) maps a merge row to its
+// slot (the rescan rows of a round)
+struct ListOut {
+  uint64_t *ukey;    // [U][KL] keys, best first
+  int32_t *unode;    // [U][KL] their nodes
+  int32_t *ucnt;     // [U] listed keys
+  uint64_t *ubound;  // [U] every unlisted node's key is below it; 0 = all listed
+  const int32_t *rslot;
+  int32_t kout;
 };
 
 // Scoring constants copied into kernel arguments (wave-uniform -> SGPRs).
@@ -148,6 +166,16 @@ struct DevState {
   int32_t *cnt = nullptr;
   void *temp = nullptr;         // rocprim temporary storage
   size_t temp_bytes = 0;
+  // incremental candidate phase (kp_incr.hip): per unit its top-KL list, per
+  // node the serial of the last round whose passes changed its usage, per
+  // round parity the changed nodes (compacted at the round start) and the
+  // rows to rescan; npos = canonical position of each node (the tie key)
+  uint64_t *ukey = nullptr, *ubound = nullptr;  // [U][KL], [U]
+  int32_t *unode = nullptr, *ucnt = nullptr;    // [U][KL], [U]
+  int32_t *chg = nullptr;                       // [N]
+  int32_t *clist = nullptr;                     // [2][N]
+  int32_t *npos = nullptr;                      // [N]
+  int32_t *rs_slot = nullptr, *rs_unit = nullptr;  // [U]
   // dist exchange
   int32_t *xg_counts = nullptr; // [world]
   int32_t *xg_send = nullptr;   // [Umax*(K+1)]
@@ -209,6 +237,20 @@ struct kp_ctx {
   int32_t pass_loop_form = 2;  // KP_PASS_LOOP_FORM: 2 register-resident (k_pass_loop2), 1 reloading
   // KP_COMPACT_MAX: largest unit range compacted by the one-workgroup kernel
   int32_t compact_max = 262144;
+  // incremental candidate phase (KP_INCR=1; a measured alternative, off by
+  // default): rounds after the first re-score only the nodes the previous
+  // round changed against per-unit top-KL lists; more changed nodes than
+  // N / incr_cthr_div rescan. Bit-identical, but the herded rounds consume
+  // the very nodes every list holds, so most rows are rescanned anyway
+  // (profiles/r03_incr_*)
+  bool incr_enabled = false;
+  int32_t incr_cthr_div = 8;
+  bool incr_trace = false;  // KP_INCR_TRACE=1: per-round changed / rescanned counts on stderr (syncs)
+  int32_t cap_incr_U = 0, cap_incr_KL = 0;
+  int32_t round_serial = 0;  // rounds enqueued on this context (the usage-change stamps)
+  int32_t cur_serial = 0;    // this round's stamp (k_accept marks changed nodes with it)
+  bool incr_active = false;  // the current solve runs the incremental phase
+  int32_t incr_round = 0;    // its current round (0: full scan)
   bool round_begin = true;  // KP_ROUND_BEGIN=0: round start + compaction as two launches
   // KP_KEYS_MERGE=0: k_csr_keys as its own launch; keys_in_merge: this
   // round's merge did its work
@@ -291,8 +333,18 @@ int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit,
                   const int32_t *rows_dev = nullptr);
 // fused filter + score + top-K of the solve (kp_topk.hip): candidates of
 // `rows` rows (act_local order) straight into cand, no score matrix
+// (lo.ukey: list mode of the incremental phase; init_wgs: the merge's extra
+// workgroups re-initialise the round state when it does k_csr_keys' work)
 int launch_score_topk(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
-                      int32_t ksh, int32_t *cand, const int32_t *rows_dev = nullptr);
+                      int32_t ksh, int32_t *cand, const int32_t *rows_dev, const ListOut &lo,
+                      bool init_wgs);
+// incremental candidate update of round `round` (>= 1, kp_incr.hip): slots
+// [0, rows) (device count rows_dev) against their units' lists and the nodes
+// the previous round changed; completed slots get their candidates (and, with
+// keys, k_csr_keys' work), the others go to the round's rescan list
+// (rs_slot / rs_unit, count counters[kRsCount + round % 2])
+int launch_cand_update(kp_ctx *c, const ScoreParams &sp, int32_t KL, int32_t rows,
+                       const int32_t *rows_dev, int32_t round, bool keys);
 int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev = nullptr);
 // this round's index form (counting or sort) and its bitmap; called by
 // launch_csr_build, or before the candidate merge when that does k_csr_keys' work

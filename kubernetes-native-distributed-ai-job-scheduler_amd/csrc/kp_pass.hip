@@ -787,6 +787,10 @@ struct AcceptOut {
   uint8_t *open;
   int32_t *status, *job_node, *job_score;
   int32_t *sdone;  // k_pass_loop: a placed slot is closed here instead of open[]
+  // incremental candidate phase: chg[node] = serial for every node whose
+  // usage this round changes (a plain store, nothing waits on it)
+  int32_t *chg;
+  int32_t serial;
 };
 
 // all-or-nothing commit of a multi-node gang by the wave that accepted its
@@ -798,11 +802,15 @@ constexpr int kGangPreN = kGangPre > 0 ? kGangPre : 1;
 template <int D>
 __device__ __forceinline__ void commit_part(const AcceptOut &o, int32_t lead, const int4 &g,
                                             const int64_t (&qq)[D]) {
+  bool any = false;
 #pragma unroll
   for (int d = 0; d < D; ++d)
-    if (qq[d] != 0)
+    if (qq[d] != 0) {
       atomicAdd(reinterpret_cast<unsigned long long *>(&o.used[(int64_t)d * o.N + g.x]),
                 (unsigned long long)((int64_t)g.y * qq[d]));
+      any = true;
+    }
+  if (any && o.chg) o.chg[g.x] = o.serial;
   for (int m = 0; m < g.y; ++m) {
     o.job_node[lead + g.z + m] = g.x;
     o.job_score[lead + g.z + m] = g.w;
@@ -1022,13 +1030,16 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
     }
   }
   // fold the single-node units committed by this wave into `used`
+  bool any = false;
 #pragma unroll
   for (int d = 0; d < D; ++d) {
     const int64_t tot = (int64_t)readlane_nt((NT)(scan_excl<N32>(add[d]) + add[d]), 63);
     if (lane == 63 && tot != 0)
       atomicAdd(reinterpret_cast<unsigned long long *>(&o.used[(int64_t)d * N + node]),
                 (unsigned long long)tot);
+    any |= tot != 0;
   }
+  if (lane == 63 && any && o.chg) o.chg[node] = o.serial;
 }
 
 // One wave per node: the nodes with bidders this round (use_list: their
@@ -1423,13 +1434,16 @@ __device__ __forceinline__ void accept_reg_pass(const AccArgs &ac, AccReg<D, N32
       decide_window<D, N32, true>(wv[t], rem, add, lane, n.node, o);
     }
   }
+  bool any = false;
 #pragma unroll
   for (int d = 0; d < D; ++d) {
     const int64_t tot = (int64_t)readlane_nt((NT)(scan_excl<N32>(add[d]) + add[d]), 63);
     if (lane == 63 && tot != 0)
       atomicAdd(reinterpret_cast<unsigned long long *>(&o.used[(int64_t)d * N + n.node]),
                 (unsigned long long)tot);
+    any |= tot != 0;
   }
+  if (lane == 63 && any && o.chg) o.chg[n.node] = o.serial;
 }
 
 template <int D, int G, bool N32, int WPB>
@@ -1600,6 +1614,8 @@ static AccArgs acc_args(kp_ctx *c, const ScoreParams &sp, int64_t P) {
   o.job_node = c->d.job_node;
   o.job_score = c->d.job_score;
   o.sdone = c->d.sdone;
+  o.chg = c->incr_active ? c->d.chg : nullptr;
+  o.serial = c->cur_serial;
   ac.pp = c->d.fz_prof ? c->d.fz_prof + 16 : nullptr;
   ac.st = c->d.stats;
   return ac;

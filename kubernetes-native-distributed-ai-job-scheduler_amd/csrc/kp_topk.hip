@@ -556,31 +556,11 @@ void k_score_topk(
 // max of the heads, and only the owner of the max advances its list (one LDS
 // read). K x (one wave max + one LDS read) per row instead of K passes over
 // all ntiles*K keys. Dynamic LDS: 4 rows x ntiles*K keys.
-// k_csr_keys' per-round state reset, thread t of the merge's extra workgroups
-// (rk.enabled): round statistics, the previous round's productive passes,
-// node segments / flags, window flags
-__device__ __forceinline__ void round_keys_init(const RoundKeys &rk, int64_t t) {
-  if (t == 0) {
-    const int32_t Aa = rk.A_dev ? min(rk.A, *rk.A_dev) : rk.A;
-    if (Aa > 0) {
-      rk.st->rounds += 1;
-      rk.st->active_sum += Aa;
-    }
-    *rk.nl_count = 0;
-  }
-  if (t < rk.N) {
-    rk.seg_start[t] = -1;
-    rk.node_flag[t] = -1;
-  }
-  if (t < rk.nwin) rk.win[t] = -1;
-  if (t < 64) {
-    if (rk.pass_flag[t] != 0)
-      atomicAdd(reinterpret_cast<unsigned long long *>(&rk.st->passes), 1ull);
-    rk.pass_flag[t] = 0;
-    if (t == 0) rk.pass_flag[kLoopBar] = 0;  // the pass loop's barrier counter
-  }
-}
-
+// List mode (lo.ukey, the incremental candidate phase, kp_incr.hip): K is the
+// list length KL >= the solve's n_cand (lo.kout); the row's top-KL keys and
+// nodes, their count and the bound (the KL-th key, 0 = every feasible node is
+// listed) go to the unit's list, the first kout nodes to cand at the row's
+// slot (lo.rslot: row -> slot, the rescan rows of a round).
 template <int LPL>
 __global__ __launch_bounds__(64 * KP_MERGE_WPB) void k_merge_tour(ScoreParams sp, const uint64_t *__restrict__ part,
                                                     int32_t ntiles,
@@ -588,7 +568,8 @@ __global__ __launch_bounds__(64 * KP_MERGE_WPB) void k_merge_tour(ScoreParams sp
                                                     const uint32_t *__restrict__ salt, int32_t rows,
                                                     const int32_t *__restrict__ rows_dev,
                                                     const int32_t *__restrict__ perm,
-                                                    int32_t *__restrict__ cand, RoundKeys rk) {
+                                                    int32_t *__restrict__ cand, RoundKeys rk,
+                                                    ListOut lo) {
   extern __shared__ uint64_t slist[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int rblocks = (rows + kMergeWPB - 1) / kMergeWPB;
@@ -613,13 +594,14 @@ __global__ __launch_bounds__(64 * KP_MERGE_WPB) void k_merge_tour(ScoreParams sp
     h[j] = 0;
     v[j] = t < ntiles ? L[t * K] : 0ull;
   }
-  const uint32_t sl = sp.tie_rotated ? salt[rows_unit[row]] : 0u;
+  const int32_t unit = rows_unit[row];
+  const uint32_t sl = sp.tie_rotated ? salt[unit] : 0u;
   const uint32_t inv = sp.tie_rotated ? kTieMulInv : 1u;
-  int32_t *out = cand + (int64_t)row * K;
   // lane it keeps the canonical position of candidate it; the positions are
   // mapped to nodes after the loop with ONE load per lane (a perm load + store
   // inside the loop serialises K memory latencies)
-  int32_t mypos = -1;
+  int32_t mypos = -1, got = 0;
+  uint64_t mykey = 0;
   for (int it = 0; it < K; ++it) {
     uint64_t b = v[0];
 #pragma unroll
@@ -635,28 +617,39 @@ __global__ __launch_bounds__(64 * KP_MERGE_WPB) void k_merge_tour(ScoreParams sp
         ++h[j];
         v[j] = h[j] < K ? L[t * K + h[j]] : 0ull;
       }
-    if (lane == it) mypos = key_node(m, sl, inv);
+    if (lane == it) {
+      mypos = key_node(m, sl, inv);
+      mykey = m;
+    }
+    got = it + 1;
   }
   // canonical position -> node (a position is always < N)
   const int32_t mine = (uint32_t)mypos < (uint32_t)sp.N ? perm[mypos] : -1;
-  if (lane < K) out[lane] = mine;
-  if (rk.enabled) {  // k_csr_keys' work for slot `row` (single GPU: slot = row)
+  const int kout = lo.ukey ? lo.kout : K;
+  const int32_t slot = lo.rslot ? lo.rslot[row] : row;
+  if (lane < kout) cand[(int64_t)slot * kout + lane] = mine;
+  if (lo.ukey) {
+    // the list: a bound below every unlisted node's key, or 0 when fewer than
+    // K keys exist (some tile ran out: every feasible node is listed)
+    const int64_t lb = (int64_t)unit * K;
     if (lane < K) {
-      rk.bid[(int64_t)row * K + lane] = 0xFFFFFFFFu;  // kNoBid
-      if (mine >= 0) atomicOr(&rk.bm[(int64_t)mine * rk.Wb + (row >> 5)], 1u << (row & 31));
+      lo.ukey[lb + lane] = mykey;
+      lo.unode[lb + lane] = mine;
     }
-    const int32_t first = __shfl(mine, 0, 64);
+    const uint64_t bound = got == K ? (uint64_t)readlane_i64((int64_t)mykey, K - 1) : 0ull;
     if (lane == 0) {
-      rk.open[row] = first >= 0 ? 1 : 0;
-      if (first < 0) rk.status[rows_unit[row]] = kNoFit;
+      lo.ucnt[unit] = got;
+      lo.ubound[unit] = bound;
     }
   }
+  if (rk.enabled) round_keys_slot(rk, slot, unit, kout, mine, lane);  // k_csr_keys' work for the slot
 }
 
 template <int D>
 struct TopkL {
   static int run(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
-                 int32_t ksh, int32_t *cand, const int32_t *rows_dev) {
+                 int32_t ksh, int32_t *cand, const int32_t *rows_dev, const ListOut &lo,
+                 bool init_wgs) {
     const int P = c->fz_P, ntiles = P / kFzTile;
     const int64_t want = ((int64_t)rows * ntiles + c->fz_wg_target - 1) / c->fz_wg_target;
     const int rpb = (int)std::min<int64_t>(kFzMaxRows, std::max<int64_t>(kFzRC, want));
@@ -678,12 +671,14 @@ struct TopkL {
     if (c->fz_end_event) KP_HIP(hipEventRecord(c->fz_end_event, c->stream));
     const int M = ntiles * sp.n_cand;
     RoundKeys rk{};
-    if (c->keys_in_merge) rk = round_keys_args(c, rows, sp.n_cand, rows_dev);
-    const dim3 mg(blocks(rows, kMergeWPB) + (rk.enabled ? blocks(rk.init_n, 64 * kMergeWPB) : 0));
+    // the slots' keys work uses the solve's K (lo.kout in list mode)
+    if (c->keys_in_merge) rk = round_keys_args(c, rows, lo.ukey ? lo.kout : sp.n_cand, c->d.counters);
+    const dim3 mg(blocks(rows, kMergeWPB) +
+                  (rk.enabled && init_wgs ? blocks(rk.init_n, 64 * kMergeWPB) : 0));
     const size_t lds = (size_t)kMergeWPB * M * sizeof(uint64_t);  // <= 16 KB per row (M <= 2,048)
 #define KP_MG(LPL)                                                                       \
   hipLaunchKernelGGL((k_merge_tour<LPL>), mg, dim3(64 * kMergeWPB), lds, c->stream, sp, c->d.part, \
-                     ntiles, rows_unit, c->d.salt, rows, rows_dev, c->d.perm, cand, rk)
+                     ntiles, rows_unit, c->d.salt, rows, rows_dev, c->d.perm, cand, rk, lo)
     if (ntiles <= 64)
       KP_MG(1);
     else if (ntiles <= 128)
@@ -705,9 +700,10 @@ struct TopkL {
 }  // namespace
 
 int launch_score_topk(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
-                      int32_t ksh, int32_t *cand, const int32_t *rows_dev) {
+                      int32_t ksh, int32_t *cand, const int32_t *rows_dev, const ListOut &lo,
+                      bool init_wgs) {
   if (rows <= 0 || c->N == 0) return KP_OK;
-  return dispatch_D<TopkL>(c->D, c, sp, rows_unit, rows, ksh, cand, rows_dev);
+  return dispatch_D<TopkL>(c->D, c, sp, rows_unit, rows, ksh, cand, rows_dev, lo, init_wgs);
 }
 
 }  // namespace kp

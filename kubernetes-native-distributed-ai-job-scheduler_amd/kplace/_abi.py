@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-KP_ABI_VERSION = 4
+KP_ABI_VERSION = 5
 KP_MAX_DIMS = 8
 KP_MAX_CAND = 32
 KP_MAX_GANG = 64
@@ -95,6 +95,7 @@ class Timing(C.Structure):
         ("select_ms", C.c_double), ("accept_ms", C.c_double),
         ("score_launches", C.c_int64), ("score_bytes", C.c_int64),
         ("select_bytes", C.c_int64), ("fused", C.c_int32), ("loop_rounds", C.c_int32),
+        ("incr_rounds", C.c_int32), ("pad", C.c_int32),
     ]
 
 
