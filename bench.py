@@ -402,7 +402,7 @@ def main():
     fused = bool(tm["fused"])
     kname = "k_score_topk" if fused else "k_score32"
     traffic, traffic_src, valu = None, None, None
-    for pmc in ("r02_pmc.json", "r01_pmc.json"):  # HBM-side bytes per launch (rocprofv3 PMC)
+    for pmc in ("r03_pmc.json", "r02_pmc.json", "r01_pmc.json"):  # HBM-side bytes per launch (rocprofv3 PMC), newest first
         path = os.path.join(REPO, "profiles", pmc)
         if os.path.exists(path):
             with open(path) as f:
@@ -415,18 +415,22 @@ def main():
         # SURVEY §8(d) honesty clause: the fused kernel never writes the
         # matrix, so its HBM fraction is on compulsory bytes only; it is
         # judged on pairs/s and on the VALU roofline (lane-ops per pair from
-        # the SQ_INSTS_VALU counter of the same solve, profiles/r02_valu.json)
-        path = os.path.join(REPO, "profiles", "r02_valu.json")
-        opp = None
-        if os.path.exists(path):
-            with open(path) as f:
-                opp = json.load(f)["kernels"].get(kname, {}).get("valu_lane_ops_per_pair")
+        # the SQ_INSTS_VALU counter of the same solve, profiles/r0N_valu.json)
+        opp, vsrc = None, None
+        for vj in ("r03_valu.json", "r02_valu.json"):  # newest evidence first
+            path = os.path.join(REPO, "profiles", vj)
+            if os.path.exists(path):
+                with open(path) as f:
+                    opp = json.load(f)["kernels"].get(kname, {}).get("valu_lane_ops_per_pair")
+                if opp:
+                    vsrc = vj
+                    break
         score_s = score_ms / 1e3 / max(args.steps, 1)  # per solve
         kpairs = st["pairs"] / score_s if score_s > 0 else 0.0
         valu = {"bound": "valu", "kernel": kname, "unit": "Tops/s (int32 lane-ops)",
                 "peak": VALU_PEAK_TOPS, "pairs_per_s_kernel": kpairs,
                 "lane_ops_per_pair": opp,
-                "lane_ops_source": "profiles/r02_valu.json (SQ_INSTS_VALU x 64 / pairs, tools/gpu_evidence.sh)"}
+                "lane_ops_source": f"profiles/{vsrc} (SQ_INSTS_VALU x 64 / pairs, tools/gpu_evidence.sh)"}
         if opp:
             valu["achieved"] = kpairs * opp / 1e12
             valu["frac"] = valu["achieved"] / VALU_PEAK_TOPS

@@ -117,6 +117,31 @@ for n, d in pmc.items():
         lds["kernels"][n] = {"bank_conflict_cycles": bc, "lds_active_cycles": act,
                              "conflict_frac": bc / act if act else None,
                              "lds_insts": sum(d.get("SQ_INSTS_LDS", [0]))}
+# score + threshold stages alone (the no-select build, round 0 only): the
+# select phase's VALU / SALU per pair is the full kernel's minus these
+ns = os.path.join(src, "pmc", "SQ_NOSEL", "run_counter_collection.csv")
+if os.path.exists(ns) and "k_score_topk" in valu["kernels"]:
+    tot = collections.defaultdict(float)
+    for r in csv.DictReader(open(ns)):
+        if kname(r["Kernel_Name"]) == "k_score_topk":
+            tot[r["Counter_Name"]] += float(r["Counter_Value"])
+    rows0 = bench.get("config", {}).get("units")  # round 0 scores every unit
+    N = bench.get("config", {}).get("nodes")
+    full = valu["kernels"]["k_score_topk"]["per_solve"]
+    if rows0 and N and pairs and tot.get("SQ_INSTS_VALU"):
+        p0 = float(rows0) * N
+        split = {"source": "SQ pass of the no-select build (KP_FZ_EXP=1, round 0: units x nodes pairs) "
+                           "vs the full kernel's SQ pass over the whole solve",
+                 "pairs_no_select_run": p0, "pairs_full_solve": pairs,
+                 "score_and_threshold": {"valu_lane_ops_per_pair": 64 * tot["SQ_INSTS_VALU"] / p0,
+                                         "salu_per_pair_x64": 64 * tot.get("SQ_INSTS_SALU", 0) / p0,
+                                         "lds_per_pair_x64": 64 * tot.get("SQ_INSTS_LDS", 0) / p0},
+                 "whole_kernel": {"valu_lane_ops_per_pair": 64 * full["SQ_INSTS_VALU"] / pairs,
+                                  "salu_per_pair_x64": 64 * full.get("SQ_INSTS_SALU", 0) / pairs,
+                                  "lds_per_pair_x64": 64 * full.get("SQ_INSTS_LDS", 0) / pairs}}
+        split["select"] = {k: split["whole_kernel"][k] - split["score_and_threshold"][k]
+                           for k in split["whole_kernel"]}
+        json.dump(split, open(os.path.join(prof, f"{rnd}_valu_split.json"), "w"), indent=1)
 for name, obj in (("pmc", hbm), ("valu", valu), ("lds", lds)):
     if obj["kernels"]:
         json.dump(obj, open(os.path.join(prof, f"{rnd}_{name}.json"), "w"), indent=1)

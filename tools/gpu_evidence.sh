@@ -37,9 +37,19 @@ pmc FETCH_SIZE FETCH_SIZE || exit $?
 pmc WRITE_SIZE WRITE_SIZE || exit $?
 pmc SQ1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY || exit $?
 pmc LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVES || exit $?
+# the same SQ pass on a k_score_topk build without its select phase
+# (tools/build_variant.sh WORKTREE noselect -DKP_FZ_EXP=1): score + threshold
+# stages alone; the select phase is the difference (its round 0 only: no
+# candidates, the solve ends after one round)
+NOSEL=kubernetes-native-distributed-ai-job-scheduler_amd/build/ab/noselect.so
+if [ -f $NOSEL ]; then
+  export KPLACE_LIB=$PWD/$NOSEL
+  pmc SQ_NOSEL SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY || exit $?
+  unset KPLACE_LIB
+fi
 timeout -k 10 300 rocprofv3 --hip-runtime-trace --kernel-trace --output-format csv -d $OUT/rt -o run -- python3 tools/place_steps.py > $OUT/rt/place.log 2>&1 || exit $?
 echo rt ok
-python3 tools/evidence_summary.py ${ROUND:-r02} $OUT $OUT/summary && ls $OUT/summary
+python3 tools/evidence_summary.py ${ROUND:-r03} $OUT $OUT/summary && ls $OUT/summary
 # the raw traces exceed what gpurun copies back: keep logs and summaries only
 rm -f $OUT/prof/run_kernel_trace.csv $OUT/prof45/run_kernel_trace.csv $OUT/*/*/run_counter_collection.csv $OUT/*/*/run_kernel_trace.csv
 du -sh $OUT
