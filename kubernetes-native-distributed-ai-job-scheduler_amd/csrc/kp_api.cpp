@@ -359,6 +359,7 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = knob("KP_INCR")) c->incr_enabled = std::atoi(e) != 0;
   if (const char *e = knob("KP_INCR_CTHR_DIV")) c->incr_cthr_div = std::max(1, std::atoi(e));
   if (const char *e = knob("KP_INCR_TRACE")) c->incr_trace = std::atoi(e) != 0;
+  if (const char *e = knob("KP_PREEMPT32")) c->preempt32 = std::atoi(e) != 0;
   if (const char *e = knob("KP_ACC_LIST")) c->acc_list = std::atoi(e);
   if (const char *e = knob("KP_PASS_LOOP")) c->pass_loop_enabled = std::atoi(e) != 0;
   if (const char *e = knob("KP_PASS_LOOP_FORM")) c->pass_loop_form = std::atoi(e) == 1 ? 1 : 2;
@@ -1613,6 +1614,16 @@ int kp_load_running(kp_ctx *c, int32_t R, const int32_t *node, const int64_t *re
                         hipMemcpyHostToDevice, c->stream));
   KP_HIP(hipStreamSynchronize(c->stream));
   c->R = R;
+  {  // k_preempt_t's packed key bounds
+    int64_t worst = 0, maxrun = 0;
+    for (int32_t n = 0; n < N; ++n) {
+      int64_t sp = 0, sn = 0;
+      for (int32_t e = off[n]; e < off[n + 1]; ++e) (rprio[e] > 0 ? sp : sn) += rprio[e];
+      worst = std::max(worst, std::max(sp, -sn));
+      maxrun = std::max<int64_t>(maxrun, off[n + 1] - off[n]);
+    }
+    c->pre_key_ok = N < (1 << 20) && maxrun < (1 << 11) && worst < ((int64_t)1 << 31);
+  }
   return KP_OK;
 }
 

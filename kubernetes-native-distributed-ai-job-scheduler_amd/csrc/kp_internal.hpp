@@ -245,7 +245,11 @@ struct kp_ctx {
   // (profiles/r03_incr_*)
   bool incr_enabled = false;
   int32_t incr_cthr_div = 8;
-  bool incr_trace = false;  // KP_INCR_TRACE=1: per-round changed / rescanned counts on stderr (syncs)
+  bool incr_trace = false;
+  bool preempt32 = true;  // KP_PREEMPT32=0: the 64-bit per-row preemption kernel on 32-bit tables too
+  // the victim pool's (victims, priority sum, node) fits one ordered 64-bit
+  // key (N < 2^20, < 2^11 running jobs per node, |sum of their priorities| < 2^31)
+  bool pre_key_ok = false;  // KP_INCR_TRACE=1: per-round changed / rescanned counts on stderr (syncs)
   int32_t cap_incr_U = 0, cap_incr_KL = 0;
   int32_t round_serial = 0;  // rounds enqueued on this context (the usage-change stamps)
   int32_t cur_serial = 0;    // this round's stamp (k_accept marks changed nodes with it)

@@ -136,6 +136,155 @@ __global__ __launch_bounds__(256) void k_preempt(int32_t N, int32_t U, int32_t P
   }
 }
 
+// Tiled 32-bit form (every cap and request < 2^32, so a node's free capacity
+// plus all its running requests stays below its capacity; and (victims,
+// cost, node) packs into one ordered 64-bit key, kp_load_running checks the
+// bounds). A workgroup owns kPtRows preemptor rows (requests in LDS) and
+// sweeps the nodes in tiles of 256, one node per thread: the node's free
+// capacity and up to kPreRun running jobs (priority, request) are loaded into
+// registers ONCE per tile and evaluated against every row of the block, so
+// the node table is read once per kPtRows rows. Per row and tile a wave
+// minimum of the packed keys (DPP) and a 4-wave merge into the row's running
+// best in LDS. Nodes with more running jobs walk their list in global memory.
+// Same order and tie rules as k_preempt: fewest victims, lowest victim
+// priority sum, lowest node index.
+constexpr int kPtRows = 128;  // preemptor rows per workgroup
+constexpr int kPreRun = 8;    // running jobs per node held in registers
+
+__device__ __forceinline__ uint64_t pre_key(int32_t cnt, int64_t cost, int32_t node) {
+  return ((uint64_t)cnt << 52) | ((uint64_t)(cost + ((int64_t)1 << 31)) << 20) | (uint64_t)node;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_preempt_t(int32_t N, int32_t U, int32_t P, int32_t R,
+                                                   const int32_t *__restrict__ plist,
+                                                   const int64_t *__restrict__ q,
+                                                   const int32_t *__restrict__ uprio,
+                                                   const int32_t *__restrict__ leader,
+                                                   const int64_t *__restrict__ cap,
+                                                   const int64_t *__restrict__ used,
+                                                   const int32_t *__restrict__ roff,
+                                                   const int64_t *__restrict__ rreq,
+                                                   const int64_t *__restrict__ rsuf,
+                                                   const int32_t *__restrict__ rprio,
+                                                   int32_t *__restrict__ out_node,
+                                                   int32_t *__restrict__ out_vict,
+                                                   int64_t *__restrict__ out_cost) {
+  __shared__ uint32_t sq[kPtRows][D];
+  __shared__ int32_t spr[kPtRows];
+  __shared__ uint64_t sbest[kPtRows];
+  __shared__ uint64_t swb[kPtRows][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r0 = blockIdx.x * kPtRows;
+  const int nrows = min(kPtRows, P - r0);
+  for (int i = tid; i < nrows * D; i += 256) {
+    const int rr = i / D, d = i % D;
+    sq[rr][d] = (uint32_t)q[(int64_t)d * U + plist[r0 + rr]];
+  }
+  for (int i = tid; i < nrows; i += 256) {
+    spr[i] = uprio[plist[r0 + i]];
+    sbest[i] = ~0ull;
+  }
+  __syncthreads();
+  for (int t0 = 0; t0 < N; t0 += 256) {
+    const int n = t0 + tid;
+    const bool valid = n < N;
+    const int32_t e0 = valid ? roff[n] : 0, e1 = valid ? roff[n + 1] : 0, cnt = e1 - e0;
+    uint32_t fr[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      fr[d] = valid ? (uint32_t)(cap[(int64_t)d * N + n] - used[(int64_t)d * N + n]) : 0u;
+    const bool shortl = cnt <= kPreRun;
+    int32_t pr[kPreRun];
+    uint32_t rq[kPreRun][D];
+#pragma unroll
+    for (int k = 0; k < kPreRun; ++k) {
+      const bool v = shortl && k < cnt;
+      pr[k] = v ? rprio[e0 + k] : INT32_MAX;  // padding: never evictable
+#pragma unroll
+      for (int d = 0; d < D; ++d) rq[k][d] = v ? (uint32_t)rreq[(int64_t)d * R + e0 + k] : 0u;
+    }
+    for (int rr = 0; rr < nrows; ++rr) {
+      const int32_t p = spr[rr];
+      uint32_t qd[D], av[D];
+      // free + every evictable request (priority < p): from the registers, or
+      // the suffix sum of a long list past its non-evictable prefix
+      int32_t f = e0;
+      if (!shortl)
+        while (f < e1 && rprio[f] >= p) ++f;  // evictable = [f, e1)
+      bool ok = valid;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        qd[d] = sq[rr][d];
+        av[d] = fr[d];
+        if (shortl) {
+#pragma unroll
+          for (int k = 0; k < kPreRun; ++k) av[d] += pr[k] < p ? rq[k][d] : 0u;
+        } else {
+          av[d] += f < e1 ? (uint32_t)rsuf[(int64_t)d * R + f] : 0u;
+        }
+        ok &= qd[d] <= av[d];
+      }
+      if (__ballot(ok) == 0) {  // no node of this wave qualifies for the row (wave-uniform)
+        if (lane == 0) swb[rr][wave] = ~0ull;
+        continue;
+      }
+      int32_t vc = 0;
+      int64_t cost = 0;
+      if (shortl) {
+        // reprieve walk in (priority desc, running index asc) order
+#pragma unroll
+        for (int k = 0; k < kPreRun; ++k) {
+          bool spare = true;
+#pragma unroll
+          for (int d = 0; d < D; ++d) spare &= qd[d] <= av[d] - rq[k][d];
+          const bool ev = ok && pr[k] < p;
+#pragma unroll
+          for (int d = 0; d < D; ++d) av[d] -= ev && spare ? rq[k][d] : 0u;
+          vc += ev && !spare ? 1 : 0;
+          cost += ev && !spare ? pr[k] : 0;
+        }
+      } else {  // a long victim list: walk it in global memory
+        for (int32_t e = f; ok && e < e1; ++e) {
+          uint32_t x[D];
+          bool spare = true;
+#pragma unroll
+          for (int d = 0; d < D; ++d) {
+            x[d] = (uint32_t)rreq[(int64_t)d * R + e];
+            spare &= qd[d] <= av[d] - x[d];
+          }
+          if (spare) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) av[d] -= x[d];
+          } else {
+            ++vc;
+            cost += rprio[e];
+          }
+        }
+      }
+      const uint64_t key = ok ? pre_key(vc, cost, n) : ~0ull;
+      const uint64_t m = ~wave_max_u64_dpp(~key);  // the wave's smallest key
+      if (lane == 0) swb[rr][wave] = m;
+    }
+    __syncthreads();
+    for (int rr = tid; rr < nrows; rr += 256) {
+      uint64_t b = sbest[rr];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) b = swb[rr][w] < b ? swb[rr][w] : b;
+      sbest[rr] = b;
+    }
+    __syncthreads();  // swb is rewritten by the next tile
+  }
+  for (int rr = tid; rr < nrows; rr += 256) {
+    const uint64_t b = sbest[rr];
+    const int32_t j = leader[plist[r0 + rr]];
+    const bool has = b != ~0ull;
+    out_node[j] = has ? (int32_t)(b & 0xFFFFFull) : -1;
+    out_vict[j] = has ? (int32_t)(b >> 52) : 0;
+    out_cost[j] = has ? (int64_t)((b >> 20) & 0xFFFFFFFFull) - ((int64_t)1 << 31) : 0;
+  }
+}
+
 __global__ void k_preempt_flags(const int32_t *__restrict__ status,
                                 const int32_t *__restrict__ size, int32_t U,
                                 int32_t *__restrict__ flag) {
@@ -155,6 +304,14 @@ __global__ void k_preempt_init(int32_t J, int32_t *__restrict__ node, int32_t *_
 template <int D>
 struct PreemptL {
   static int run(kp_ctx *c, int32_t P) {
+    if (c->fits32 && c->preempt32 && c->pre_key_ok) {
+      hipLaunchKernelGGL((k_preempt_t<D>), dim3(blocks(P, kPtRows)), dim3(256), 0, c->stream, c->N,
+                         c->U, P, c->R, c->d.plist, c->d.q, c->d.uprio, c->d.leader, c->d.cap,
+                         c->d.used, c->d.roff, c->d.rreq, c->d.rsuf, c->d.rprio, c->d.pre_node,
+                         c->d.pre_vict, c->d.pre_cost);
+      KP_HIP(hipGetLastError());
+      return KP_OK;
+    }
     hipLaunchKernelGGL((k_preempt<D>), dim3(blocks(P, kPreRows)), dim3(256), 0, c->stream, c->N,
                        c->U, P, c->R, c->d.plist, c->d.q, c->d.uprio, c->d.leader, c->d.cap,
                        c->d.used, c->d.roff, c->d.rreq, c->d.rsuf, c->d.rprio, c->d.pre_node,

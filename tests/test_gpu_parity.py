@@ -630,6 +630,55 @@ def test_preempt_config4_parity(oracle, placer):
     assert (gp["victims"][nom] >= 1).all()
 
 
+@pytest.mark.parametrize("per_node", [6, 12, 30])
+def test_preempt_long_victim_lists(oracle, placer, per_node):
+    """Up to 2 x per_node running jobs per node: nodes with more than the 8
+    that the 32-bit preemption kernel holds in registers take its per-row
+    walk over global memory, next to nodes with short lists."""
+    from test_oracle import rand_running
+    w = random_workload(777 + per_node, J=1500, N=150, used_frac=0.95)
+    rn, rq, rp = rand_running(per_node, w, per_node=2 * per_node)
+    p = _abi.default_params(score_mode=per_node % 2)
+    g, gp, o, op = _preempt_both(oracle, placer, w, p, rn, rq, rp)
+    _assert_same(g, o, f"long victim lists {per_node}")
+    _assert_same_pre(gp, op, f"long victim lists {per_node}")
+    assert np.bincount(rn, minlength=w.N).max() > 8
+
+
+def test_preempt_wide_priorities(oracle, placer):
+    """Priority sums that do not fit the tiled kernel's packed 32-bit cost
+    field (|sum| >= 2^31 on some node) take the per-row kernel; negative
+    priorities included."""
+    from test_oracle import rand_running
+    w = random_workload(4242, J=1200, N=110, used_frac=0.9)
+    rn, rq, rp = rand_running(11, w, per_node=6)
+    rp = ((rp.astype(np.int64) - 2) * (1 << 29)).astype(np.int32)
+    prio = ((w.prio.astype(np.int64) - 2) * (1 << 29) + 7).astype(np.int32)
+    w = synth.Workload(w.J, w.N, w.D, w.req, w.cap, w.used, prio, w.gang_id, w.gang_size, w.topo,
+                       name="wideprio")
+    p = _abi.default_params()
+    g, gp, o, op = _preempt_both(oracle, placer, w, p, rn, rq, rp)
+    _assert_same(g, o, "wide priorities")
+    _assert_same_pre(gp, op, "wide priorities")
+
+
+def test_preempt_kernel_forms_agree(oracle, monkeypatch):
+    """KP_PREEMPT32=0 (the per-row 64-bit kernel on a 32-bit table) gives the
+    same nominations as the default register-resident 32-bit kernel."""
+    w = synth.config4(20_000, 2_000)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[4])
+    m = w.meta
+    out = []
+    for v in ("1", "0"):
+        monkeypatch.setenv("KP_PREEMPT32", v)
+        with Placer(device=0) as pl:
+            _, gp, _, op = _preempt_both(oracle, pl, w, p, m["run_node"], m["run_req"], m["run_prio"])
+        _assert_same_pre(gp, op, f"KP_PREEMPT32={v}")
+        out.append(gp)
+    for k in ("node", "victims", "cost"):
+        assert np.array_equal(out[0][k], out[1][k])
+
+
 def test_preempt_requires_solve_and_valid_pool(placer):
     cap = np.full((4, 3), 10, np.int64)
     used = np.full((4, 3), 5, np.int64)
