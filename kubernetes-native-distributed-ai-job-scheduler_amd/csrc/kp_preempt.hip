@@ -139,17 +139,23 @@ __global__ __launch_bounds__(256) void k_preempt(int32_t N, int32_t U, int32_t P
 // Tiled 32-bit form (every cap and request < 2^32, so a node's free capacity
 // plus all its running requests stays below its capacity; and (victims,
 // cost, node) packs into one ordered 64-bit key, kp_load_running checks the
-// bounds). A workgroup owns kPtRows preemptor rows (requests in LDS) and
+// bounds). A workgroup owns kPtRows (32) preemptor rows (requests in LDS) and
 // sweeps the nodes in tiles of 256, one node per thread: the node's free
-// capacity and up to kPreRun running jobs (priority, request) are loaded into
+// capacity and up to kPreRun (16) running jobs (priority, request) are loaded into
 // registers ONCE per tile and evaluated against every row of the block, so
 // the node table is read once per kPtRows rows. Per row and tile a wave
 // minimum of the packed keys (DPP) and a 4-wave merge into the row's running
 // best in LDS. Nodes with more running jobs walk their list in global memory.
 // Same order and tie rules as k_preempt: fewest victims, lowest victim
 // priority sum, lowest node index.
-constexpr int kPtRows = 128;  // preemptor rows per workgroup
-constexpr int kPreRun = 8;    // running jobs per node held in registers
+#ifndef KP_PT_ROWS
+#define KP_PT_ROWS 32  // preemptor rows per workgroup (64: +1 ms, 128: +18 ms on config #4, tools/ab_preempt.sh)
+#endif
+#ifndef KP_PRE_RUN
+#define KP_PRE_RUN 16  // running jobs per node in registers (8: +18 ms, 12: +1 ms, 24: +19 ms)
+#endif
+constexpr int kPtRows = KP_PT_ROWS;
+constexpr int kPreRun = KP_PRE_RUN;
 
 __device__ __forceinline__ uint64_t pre_key(int32_t cnt, int64_t cost, int32_t node) {
   return ((uint64_t)cnt << 52) | ((uint64_t)(cost + ((int64_t)1 << 31)) << 20) | (uint64_t)node;

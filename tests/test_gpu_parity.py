@@ -632,8 +632,8 @@ def test_preempt_config4_parity(oracle, placer):
 
 @pytest.mark.parametrize("per_node", [6, 12, 30])
 def test_preempt_long_victim_lists(oracle, placer, per_node):
-    """Up to 2 x per_node running jobs per node: nodes with more than the 8
-    that the 32-bit preemption kernel holds in registers take its per-row
+    """Up to 2 x per_node running jobs per node: nodes with more than the 16
+    that the tiled preemption kernel holds in registers take its per-row
     walk over global memory, next to nodes with short lists."""
     from test_oracle import rand_running
     w = random_workload(777 + per_node, J=1500, N=150, used_frac=0.95)
@@ -642,7 +642,7 @@ def test_preempt_long_victim_lists(oracle, placer, per_node):
     g, gp, o, op = _preempt_both(oracle, placer, w, p, rn, rq, rp)
     _assert_same(g, o, f"long victim lists {per_node}")
     _assert_same_pre(gp, op, f"long victim lists {per_node}")
-    assert np.bincount(rn, minlength=w.N).max() > 8
+    assert np.bincount(rn, minlength=w.N).max() > (16 if per_node >= 12 else 8)
 
 
 def test_preempt_wide_priorities(oracle, placer):
