@@ -362,6 +362,7 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = knob("KP_PREEMPT32")) c->preempt32 = std::atoi(e) != 0;
   if (const char *e = knob("KP_ACC_LIST")) c->acc_list = std::atoi(e);
   if (const char *e = knob("KP_PASS_LOOP")) c->pass_loop_enabled = std::atoi(e) != 0;
+  if (const char *e = knob("KP_PASS_WG_T")) c->pass_wg_max = std::max(0, std::atoi(e));
   if (const char *e = knob("KP_PASS_LOOP_FORM")) c->pass_loop_form = std::atoi(e) == 1 ? 1 : 2;
   if (const char *e = knob("KP_PASS_LOOP_PMAX")) c->pass_loop_pmax = std::max(1, std::min(256, std::atoi(e)));
   if (const char *e = knob("KP_KEYS_MERGE")) c->keys_merge_enabled = std::atoi(e) != 0;
@@ -929,7 +930,8 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     KP_TRY(launch_csr_build(c, A, K, A_dev));
     // small rounds: every pass in one persistent launch
     bool looped = false;
-    KP_TRY(launch_pass_loop(c, sp, A, A_dev, p->max_passes, &looped));
+    KP_TRY(launch_pass_wg(c, sp, A, A_dev, p->max_passes, &looped));
+    if (!looped) KP_TRY(launch_pass_loop(c, sp, A, A_dev, p->max_passes, &looped));
     if (looped) {
       tm.loop_rounds++;
       return KP_OK;

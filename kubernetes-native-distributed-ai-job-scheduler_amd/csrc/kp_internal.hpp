@@ -233,6 +233,10 @@ struct kp_ctx {
   // KP_PASS_LOOP_PMAX: largest grid): bit-identical, but a pass costs about
   // what its two launches cost (profiles/r03_pass_loop_*)
   bool pass_loop_enabled = false;
+  // one-workgroup pass loop (k_pass_wg) for rounds of at most pass_wg_max
+  // slots (KP_PASS_WG_T; 0 = off, the default: a measured alternative,
+  // neutral at <= 256 slots and slower above, profiles/r03_pass_wg_ab.txt)
+  int32_t pass_wg_max = 0;
   int32_t pass_loop_pmax = 64;
   int32_t pass_loop_form = 2;  // KP_PASS_LOOP_FORM: 2 register-resident (k_pass_loop2), 1 reloading
   // KP_COMPACT_MAX: largest unit range compacted by the one-workgroup kernel
@@ -366,6 +370,9 @@ int launch_accept(kp_ctx *c, const ScoreParams &sp, int32_t pass, int32_t A);
 void loop_profile_dump();
 void loop_profile_reset();
 // every pass of the round in one persistent launch (*done), if the round qualifies
+// every pass of a round of at most pass_wg_max slots in ONE workgroup (*done)
+int launch_pass_wg(kp_ctx *c, const ScoreParams &sp, int32_t A, const int32_t *A_dev,
+                   int32_t max_passes, bool *done);
 int launch_pass_loop(kp_ctx *c, const ScoreParams &sp, int32_t A, const int32_t *A_dev,
                      int32_t max_passes, bool *done);
 // the static per-node plan records d.nst (every solve, after the division tables)

@@ -1522,6 +1522,53 @@ __global__ __launch_bounds__(64 * WPB) void k_pass_loop2(PlanArgs pa, AccArgs ac
   }
 }
 
+// ---- one-workgroup pass loop (k_pass_wg) -----------------------------------------
+// Every pass of a SMALL round in one 1,024-thread workgroup on one CU: plan
+// (16 waves over the slot groups) -> __syncthreads -> accept (16 waves over
+// the round's bid nodes) -> __syncthreads, until a pass without proposals or
+// max_passes. The per-pass work is k_plan's and k_accept's own device
+// functions in their launch-per-pass form (plain loads and stores, open[]):
+// within one workgroup __syncthreads orders global memory as a kernel
+// boundary does, with no grid barrier, no agent-scope hand-off and no launch
+// per phase. Only for rounds whose slots fit a few sweeps of the workgroup
+// (KP_PASS_WG_T); larger rounds need the whole GPU per pass.
+template <int D, int G, bool W32, bool N32>
+__global__ __launch_bounds__(1024) void k_pass_wg(PlanArgs pa, AccArgs ac, int32_t max_passes) {
+  constexpr int SPW = 64 / G;  // slots per wave
+  const int wave = threadIdx.x >> 6;
+  const int32_t A = pa.A_dev ? min(pa.A, *pa.A_dev) : pa.A;
+  if (A <= 0) return;  // workgroup-uniform
+  const int32_t cnt = *ac.nl_count;  // bid nodes of the round (k_csr_scan)
+  {  // k_plan pass 0's counting-mode prologue: per 64-entry window the
+     // smallest request per dim (accept's pruning bound)
+    const int32_t ptot = *pa.ptot;
+    for (int64_t w = wave; w < pa.nwin; w += 16) {
+      const int64_t e = w * 64 + (threadIdx.x & 63);
+      const bool ok = e < ptot;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        uint64_t x = ok ? (uint64_t)pa.ent_q[(int64_t)d * pa.P + e] : ~0ull;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+          const uint64_t o = shfl_xor_u64(x, m);
+          x = o < x ? o : x;
+        }
+        if ((threadIdx.x & 63) == 0) pa.winmin[(int64_t)d * pa.nwin + w] = (int64_t)x;
+      }
+    }
+  }
+  for (int32_t pass = 0; pass < max_passes; ++pass) {
+    for (int g = wave; g * SPW < A; g += 16) plan_wave<D, G, W32>(pa, pass, g);
+    __syncthreads();  // bids, window / node / pass flags (and the winmin prologue)
+    if (pa.pass_flag[pass] == 0) break;  // the same word for every wave
+    for (int i = wave; i < cnt; i += 16) {
+      const int4 r = ac.nrec[i];
+      accept_node<D, N32>(ac, pass, r.x, r.y, r.z);
+    }
+    __syncthreads();  // usage, placements, closed slots
+  }
+}
+
 // the W32 member loop's key: largest score + 64 * w_spread + 1 < 2^(32 - lb)
 static bool plan_key_ok(const ScoreParams &sp, int lb) {
   int64_t bound = (int64_t)sp.w_gpu_fit + sp.w_affinity + 64 * (int64_t)sp.w_spread + 1;
@@ -1715,6 +1762,33 @@ struct LoopL {
 };
 
 }  // namespace
+
+template <int D>
+struct PassWgL {
+  static int run(kp_ctx *c, const ScoreParams &sp, int32_t A, const int32_t *A_dev,
+                 int32_t max_passes) {
+    if constexpr (D > 4) {  // instantiated for D <= 4 only
+      return KP_ESTATE;
+    } else {
+      const PlanArgs pa = plan_args(c, sp, A, 0, A_dev);
+      const AccArgs ac = acc_args(c, sp, (int64_t)A * sp.n_cand);
+      const bool w32 = c->fits32 && plan_key_ok(sp, sp.n_cand <= 16 ? 4 : 5);
+      const bool n32 = c->fits32 && c->max_cap < ((int64_t)1 << 26);
+#define KP_PWG(G_, W_, N_) \
+  hipLaunchKernelGGL((k_pass_wg<D, G_, W_, N_>), dim3(1), dim3(1024), 0, c->stream, pa, ac, max_passes)
+      if (sp.n_cand <= 16) {
+        if (w32) { if (n32) KP_PWG(16, true, true); else KP_PWG(16, true, false); }
+        else { if (n32) KP_PWG(16, false, true); else KP_PWG(16, false, false); }
+      } else {
+        if (w32) { if (n32) KP_PWG(32, true, true); else KP_PWG(32, true, false); }
+        else { if (n32) KP_PWG(32, false, true); else KP_PWG(32, false, false); }
+      }
+#undef KP_PWG
+      KP_HIP(hipGetLastError());
+      return KP_OK;
+    }
+  }
+};
 
 // CSR sort configuration: rounds with up to KP_SORT_SINGLE_BS x KP_SORT_SINGLE_IPT
 // entries sort in one workgroup (rocprim's default: 1,024); larger ones run the
@@ -1914,6 +1988,17 @@ int launch_pass_loop(kp_ctx *c, const ScoreParams &sp, int32_t A, const int32_t 
   const int64_t P = ((int64_t)A + KP_LOOP_WPB * spw - 1) / (KP_LOOP_WPB * spw);
   if (P > c->pass_loop_pmax) return KP_OK;
   KP_TRY(dispatch_D<LoopL>(c->D, c, sp, A, A_dev, (int32_t)std::max<int64_t>(P, 1), max_passes));
+  *done = true;
+  return KP_OK;
+}
+
+int launch_pass_wg(kp_ctx *c, const ScoreParams &sp, int32_t A, const int32_t *A_dev,
+                   int32_t max_passes, bool *done) {
+  *done = false;
+  if (c->pass_wg_max <= 0 || A > c->pass_wg_max || c->csr_mode != 1 || A <= 0 || c->N <= 0 ||
+      c->D > 4)
+    return KP_OK;
+  KP_TRY(dispatch_D<PassWgL>(c->D, c, sp, A, A_dev, max_passes));
   *done = true;
   return KP_OK;
 }
