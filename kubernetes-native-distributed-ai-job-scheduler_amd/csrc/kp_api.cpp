@@ -363,6 +363,7 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = knob("KP_ACC_LIST")) c->acc_list = std::atoi(e);
   if (const char *e = knob("KP_PASS_LOOP")) c->pass_loop_enabled = std::atoi(e) != 0;
   if (const char *e = knob("KP_PASS_WG_T")) c->pass_wg_max = std::max(0, std::atoi(e));
+  if (const char *e = knob("KP_PASS_FOLLOW")) c->pass_follow = std::max(0, std::min(64, std::atoi(e)));
   if (const char *e = knob("KP_PASS_LOOP_FORM")) c->pass_loop_form = std::atoi(e) == 1 ? 1 : 2;
   if (const char *e = knob("KP_PASS_LOOP_PMAX")) c->pass_loop_pmax = std::max(1, std::min(256, std::atoi(e)));
   if (const char *e = knob("KP_KEYS_MERGE")) c->keys_merge_enabled = std::atoi(e) != 0;
@@ -388,12 +389,14 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void **>(&c->pinned), 4096, hipHostMallocDefault) !=
           hipSuccess ||
-      hipHostMalloc(reinterpret_cast<void **>(&c->pinned_coh), 64,
+      hipHostMalloc(reinterpret_cast<void **>(&c->pinned_coh), 512,
                     hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
       hipMalloc(reinterpret_cast<void **>(&c->d.dl_bad), 16 * sizeof(int32_t)) != hipSuccess) {
     kp_destroy(c);
     return KP_EHIP;
   }
+  c->hpass = c->pinned_coh + 32;
+  for (int i = 0; i < 64; ++i) c->hpass[i] = -1;  // never a tag (tags are even, >= 0)
   if (nccl_comm) {
     c->nccl_comm = nccl_comm;
   } else if (world > 1 && nccl_id) {  // else: host-staged exchange (kp_set_allgather)
@@ -925,7 +928,8 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     tm.score_launches++;
     return KP_OK;
   };
-  auto passes_of_round = [&](int32_t A, const int32_t *A_dev) -> int {
+  double pass_wait_us = 0;
+  auto passes_of_round = [&](int32_t A, const int32_t *A_dev, bool follow) -> int {
     // also opens the slots, banks + clears the pass flags
     KP_TRY(launch_csr_build(c, A, K, A_dev));
     // small rounds: every pass in one persistent launch
@@ -937,7 +941,42 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
       return KP_OK;
     }
     // passes run back to back on the device: no host round trip inside a round
+    const int32_t M = follow && A > 0 && c->N > 0 ? c->pass_follow : 0;
+    if (M == 0 || M >= p->max_passes) {
+      for (int32_t pass = 0; pass < p->max_passes; ++pass) {
+        KP_TRY(launch_plan(c, sp, A, pass, A_dev));
+        KP_TRY(launch_accept(c, sp, pass, A));
+      }
+      return KP_OK;
+    }
+    // host-followed: pass p is enqueued once pass p - M's flag (stored by its
+    // k_accept into coherent host memory, tagged with the round serial) says
+    // that pass had proposals; the first pass without any ends the round, so a
+    // round that converges early leaves at most M - 1 no-op passes behind
+    // instead of max_passes - passes
+    const int32_t tag = (int32_t)(((uint32_t)c->cur_serial & 0x3FFFFFFFu) << 1);
+    struct HpassOff {
+      kp_ctx *c;
+      ~HpassOff() { c->hpass_on = false; }
+    } hoff{c};
+    c->hpass_on = true;
     for (int32_t pass = 0; pass < p->max_passes; ++pass) {
+      if (pass >= M) {
+        const auto w0 = std::chrono::steady_clock::now();
+        const int32_t *f = c->hpass + (pass - M);
+        int32_t v;
+        for (uint32_t spin = 0; ((v = __atomic_load_n(f, __ATOMIC_ACQUIRE)) & ~1) != tag; ++spin) {
+          if ((spin & 1023u) == 1023u &&
+              std::chrono::steady_clock::now() - w0 > std::chrono::milliseconds(200)) {
+            KP_HIP(hipStreamSynchronize(c->stream));  // the stream has stored it for sure
+            v = __atomic_load_n(f, __ATOMIC_ACQUIRE);
+            if ((v & ~1) != tag) return fail(KP_EHIP, "kp_solve: pass flag not delivered");
+            break;
+          }
+        }
+        pass_wait_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - w0).count();
+        if ((v & 1) == 0) break;  // pass - M had no proposals: the round is over
+      }
       KP_TRY(launch_plan(c, sp, A, pass, A_dev));
       KP_TRY(launch_accept(c, sp, pass, A));
     }
@@ -1000,13 +1039,13 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
         for (int64_t r0 = 0; r0 < A; r0 += rpc)
           KP_TRY(score_select(r0, (int32_t)std::min<int64_t>(rpc, A - r0), nullptr, r));
         round_active.push_back(A);
-        KP_TRY(passes_of_round(A, nullptr));
+        KP_TRY(passes_of_round(A, nullptr, true));
         A_bound = A;
         continue;
       }
       const int32_t *A_dev = c->d.counters;
       KP_TRY(score_select(0, (int32_t)A_bound, A_dev, r));
-      KP_TRY(passes_of_round((int32_t)A_bound, A_dev));
+      KP_TRY(passes_of_round((int32_t)A_bound, A_dev, true));
       if (c->incr_trace && incr) {  // diagnostics: synchronous per-round counters
         int32_t h[4] = {0, 0, 0, 0};
         KP_HIP(hipMemcpyAsync(h, c->d.counters, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
@@ -1027,6 +1066,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     }
     if (c->host_prof) {
       const double tot = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h_start).count();
+      std::fprintf(stderr, "kp_host_prof pass_wait_us %.1f\n", pass_wait_us);
       std::fprintf(stderr, "kp_host_prof rounds %zu host_loop_us %.1f wait_us %.1f enqueue_us %.1f\n",
                    round_active.size(), tot, wait_us, tot - wait_us);
     }
@@ -1075,7 +1115,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
                             c->stream));
       KP_HIP(hipEventRecord(evG, c->stream));
       KP_TRY(passes_of_round((int32_t)std::min<int64_t>(U, (int64_t)B * c->world),
-                             c->d.counters + 1));
+                             c->d.counters + 1, true));
       KP_TRY(wait_event(c, evG));  // lands before this round's passes run
       round_active.push_back(*Al_h);
       G_bound = *G_h;

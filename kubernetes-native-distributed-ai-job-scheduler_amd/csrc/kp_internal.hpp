@@ -301,7 +301,13 @@ struct kp_ctx {
   int32_t *pinned = nullptr;  // small counters
   // coherent pinned word the compaction kernel stores the round's active
   // count into (KP_COUNT_DIRECT=0: copy it with hipMemcpyAsync instead)
-  int32_t *pinned_coh = nullptr;
+  int32_t *pinned_coh = nullptr;  // [0]: round count; [32, 96): per-pass flags (hpass)
+  // host-followed passes (one GPU): the host keeps pass_follow passes enqueued
+  // ahead of the last pass whose flag k_accept stored into hpass, and stops at
+  // the first pass without proposals (0 = every round enqueues max_passes)
+  int32_t *hpass = nullptr;
+  int32_t pass_follow = 2;
+  bool hpass_on = false;
   void *stage = nullptr;  // pinned staging of kp_load_jobs' unit arrays
   size_t stage_bytes = 0;
   bool count_direct = true;

@@ -945,6 +945,10 @@ struct AccArgs {
   const int64_t *winmin;
   int64_t nwin;
   AcceptOut o;
+  // host-followed passes: this pass's flag, tagged with the round serial, to
+  // coherent host memory (the host enqueues further passes only while it is set)
+  int32_t *hflag;
+  int32_t htag;
   uint64_t *pp;            // KP_PASS_PROFILE only
   const SolveStats *st;    // KP_PASS_PROFILE only (round index)
 };
@@ -1050,6 +1054,9 @@ __global__ __launch_bounds__(64 * KP_ACC_WPB) void k_accept(AccArgs ac, int32_t 
   const int wv = blockIdx.x * KP_ACC_WPB + (threadIdx.x >> 6);
   const int nw = gridDim.x * KP_ACC_WPB;  // grid-stride: the grid may be smaller than the node count
   const int32_t pf = ac.pass_flag[pass];
+  if (ac.hflag && blockIdx.x == 0 && threadIdx.x == 0)  // final: plan `pass` has ended
+    __hip_atomic_store(ac.hflag + pass, ac.htag | (pf ? 1 : 0), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
   if (use_list) {  // first record and count loaded together (nrec has 4 spare entries)
 #if KP_NREC
     const int4 r = ac.nrec[wv];
@@ -1663,6 +1670,8 @@ static AccArgs acc_args(kp_ctx *c, const ScoreParams &sp, int64_t P) {
   o.sdone = c->d.sdone;
   o.chg = c->incr_active ? c->d.chg : nullptr;
   o.serial = c->cur_serial;
+  ac.hflag = c->hpass_on ? c->hpass : nullptr;
+  ac.htag = (int32_t)(((uint32_t)c->cur_serial & 0x3FFFFFFFu) << 1);
   ac.pp = c->d.fz_prof ? c->d.fz_prof + 16 : nullptr;
   ac.st = c->d.stats;
   return ac;

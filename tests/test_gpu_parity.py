@@ -315,6 +315,27 @@ def test_pass_wg_parity(oracle, monkeypatch, T, cfg):
     _assert_same(g2, o, f"pass wg T {T} cfg {cfg}, second solve")
 
 
+@pytest.mark.parametrize("M", ["0", "1", "2", "3", "15", "16"])
+@pytest.mark.parametrize("cfg", [(3, 20_000, 2_000, 16), (4, 8_000, 1_500, 16), (2, 6_000, 600, 3)])
+def test_pass_follow_parity(oracle, monkeypatch, M, cfg):
+    """Host-followed passes (KP_PASS_FOLLOW = M): pass p is enqueued only once
+    pass p - M's flag, stored by k_accept into coherent host memory, shows
+    proposals. M = 0 and M >= max_passes enqueue every pass; M = 1 waits for
+    each pass before the next. Same placement, rounds and passes as the oracle,
+    a second solve too (the flags are tagged with the round serial, so stale
+    flags of the previous solve never end a round)."""
+    monkeypatch.setenv("KP_PASS_FOLLOW", M)
+    no, J, N, max_passes = cfg
+    w = synth.config(no, J, N)
+    p = _abi.default_params(**{**synth.CONFIG_PARAMS[no], "max_passes": max_passes})
+    with Placer(device=0) as pl:
+        g = pl.place(w, p)
+        g2 = pl.place(w, p)
+    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
+    _assert_same(g, o, f"pass follow M {M} cfg {cfg}")  # incl. rounds and passes
+    _assert_same(g2, o, f"pass follow M {M} cfg {cfg}, second solve")
+
+
 def test_pass_wg_random_parity(oracle, monkeypatch):
     """The one-workgroup loop on random snapshots: gangs spread over several
     nodes, both score modes, D <= 4, 32-candidate lists (32-lane groups)."""
