@@ -363,6 +363,7 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = knob("KP_ACC_LIST")) c->acc_list = std::atoi(e);
   if (const char *e = knob("KP_PASS_LOOP")) c->pass_loop_enabled = std::atoi(e) != 0;
   if (const char *e = knob("KP_PASS_WG_T")) c->pass_wg_max = std::max(0, std::atoi(e));
+  if (const char *e = knob("KP_ACC_BIG_RATIO")) c->acc_big_ratio = std::max(0, std::atoi(e));
   if (const char *e = knob("KP_PASS_FOLLOW")) c->pass_follow = std::max(0, std::min(64, std::atoi(e)));
   if (const char *e = knob("KP_PASS_LOOP_FORM")) c->pass_loop_form = std::atoi(e) == 1 ? 1 : 2;
   if (const char *e = knob("KP_PASS_LOOP_PMAX")) c->pass_loop_pmax = std::max(1, std::min(256, std::atoi(e)));

@@ -307,6 +307,7 @@ struct kp_ctx {
   // the first pass without proposals (0 = every round enqueues max_passes)
   int32_t *hpass = nullptr;
   int32_t pass_follow = 2;
+  int32_t acc_big_ratio = 48;  // k_accept's long-row form when A*K >= ratio * N (0: never)
   bool hpass_on = false;
   void *stage = nullptr;  // pinned staging of kp_load_jobs' unit arrays
   size_t stage_bytes = 0;

@@ -34,6 +34,9 @@
 #ifndef KP_ACC_BATCH
 #define KP_ACC_BATCH 2  // k_accept: flagged windows loaded together (2 < 4 < 8, tools/ab_mix.sh)
 #endif
+#ifndef KP_ACC_BIG
+#define KP_ACC_BIG 8  // k_accept of rounds with long bidder rows (kp_ctx::acc_big_ratio)
+#endif
 #ifndef KP_ACC_SPEC
 #define KP_ACC_SPEC 0  // 1: a bidder row's first loads issued before the node's pass flag is known (slower, tools/ab_mix.sh)
 #endif
@@ -959,7 +962,7 @@ struct AccArgs {
 // flagged windows whose smallest request no longer fits the node's remaining
 // capacity in some dim are skipped unread (a contested node fills after a
 // few windows; the rest of its long bidder row is then rejected unread).
-template <int D, bool N32, bool COH = false>
+template <int D, bool N32, bool COH = false, int B = KP_ACC_BATCH>
 __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int node, int32_t e0,
                                             int32_t e1) {
   using NT = typename Win<D, N32>::NT;
@@ -991,7 +994,7 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
     decide_window<D, N32, COH>(wv, rem, add, lane, node, o);
     KP_PP_MARK(3);
   } else {
-    constexpr int BATCH = KP_ACC_BATCH;  // flagged windows whose operands are loaded together
+    constexpr int BATCH = B;  // flagged windows whose operands are loaded together
     for (int wb = w0; wb <= w1; wb += 64) {
       const int wi = wb + lane;
       const bool mine = wi <= w1;
@@ -1049,7 +1052,7 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
 // One wave per node: the nodes with bidders this round (use_list: their
 // records {node, seg_start, seg_end}, written by plan pass 0) or every node;
 // nothing to do after a pass without proposals.
-template <int D, bool N32>
+template <int D, bool N32, int B>
 __global__ __launch_bounds__(64 * KP_ACC_WPB) void k_accept(AccArgs ac, int32_t pass, int32_t use_list) {
   const int wv = blockIdx.x * KP_ACC_WPB + (threadIdx.x >> 6);
   const int nw = gridDim.x * KP_ACC_WPB;  // grid-stride: the grid may be smaller than the node count
@@ -1062,25 +1065,25 @@ __global__ __launch_bounds__(64 * KP_ACC_WPB) void k_accept(AccArgs ac, int32_t 
     const int4 r = ac.nrec[wv];
     const int32_t cnt = *ac.nl_count;
     if (wv >= cnt || !pf) return;
-    accept_node<D, N32>(ac, pass, r.x, r.y, r.z);
+    accept_node<D, N32, false, B>(ac, pass, r.x, r.y, r.z);
     for (int i = wv + nw; i < cnt; i += nw) {
       const int4 ri = ac.nrec[i];
-      accept_node<D, N32>(ac, pass, ri.x, ri.y, ri.z);
+      accept_node<D, N32, false, B>(ac, pass, ri.x, ri.y, ri.z);
     }
 #else
     const int32_t nd = ac.node_list[wv];
     const int32_t cnt = *ac.nl_count;
     if (wv >= cnt || !pf) return;
-    accept_node<D, N32>(ac, pass, nd, ac.seg_start[nd], ac.seg_end[nd]);
+    accept_node<D, N32, false, B>(ac, pass, nd, ac.seg_start[nd], ac.seg_end[nd]);
     for (int i = wv + nw; i < cnt; i += nw) {
       const int32_t ni = ac.node_list[i];
-      accept_node<D, N32>(ac, pass, ni, ac.seg_start[ni], ac.seg_end[ni]);
+      accept_node<D, N32, false, B>(ac, pass, ni, ac.seg_start[ni], ac.seg_end[ni]);
     }
 #endif
   } else {
     if (!pf) return;
     for (int node = wv; node < ac.sp.N; node += nw)
-      accept_node<D, N32>(ac, pass, node, ac.seg_start[node], ac.seg_end[node]);
+      accept_node<D, N32, false, B>(ac, pass, node, ac.seg_start[node], ac.seg_end[node]);
   }
 }
 
@@ -1712,12 +1715,20 @@ struct AcceptL {
     int64_t waves = std::min<int64_t>(P, c->N);
     if (c->acc_waves > 0) waves = std::min<int64_t>(waves, c->acc_waves);
     // 32-bit first-fit sums while every capacity < 2^26 (64 terms stay < 2^32)
-    if (c->fits32 && c->max_cap < ((int64_t)1 << 26))
-      hipLaunchKernelGGL((k_accept<D, true>), dim3(blocks(waves, KP_ACC_WPB)), dim3(64 * KP_ACC_WPB), 0, c->stream, ac,
-                         pass, use_list);
+    const bool n32 = c->fits32 && c->max_cap < ((int64_t)1 << 26);
+    // rounds whose bidder entries average >= acc_big_ratio per node (herded,
+    // contested rows: config #4) load KP_ACC_BIG flagged windows per round
+    // trip instead of KP_ACC_BATCH; short rows lose by it
+    const bool big = c->acc_big_ratio > 0 && P >= (int64_t)c->acc_big_ratio * c->N;
+    const dim3 g(blocks(waves, KP_ACC_WPB)), b(64 * KP_ACC_WPB);
+    if (n32 && big)
+      hipLaunchKernelGGL((k_accept<D, true, KP_ACC_BIG>), g, b, 0, c->stream, ac, pass, use_list);
+    else if (n32)
+      hipLaunchKernelGGL((k_accept<D, true, KP_ACC_BATCH>), g, b, 0, c->stream, ac, pass, use_list);
+    else if (big)
+      hipLaunchKernelGGL((k_accept<D, false, KP_ACC_BIG>), g, b, 0, c->stream, ac, pass, use_list);
     else
-      hipLaunchKernelGGL((k_accept<D, false>), dim3(blocks(waves, KP_ACC_WPB)), dim3(64 * KP_ACC_WPB), 0, c->stream, ac,
-                         pass, use_list);
+      hipLaunchKernelGGL((k_accept<D, false, KP_ACC_BATCH>), g, b, 0, c->stream, ac, pass, use_list);
     KP_HIP(hipGetLastError());
     return KP_OK;
   }

@@ -336,6 +336,30 @@ def test_pass_follow_parity(oracle, monkeypatch, M, cfg):
     _assert_same(g2, o, f"pass follow M {M} cfg {cfg}, second solve")
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_accept_long_row_form_parity(oracle, monkeypatch, seed):
+    """k_accept's long-row form (KP_ACC_BIG flagged windows per load round
+    trip; chosen when A*K >= KP_ACC_BIG_RATIO * N) forced on every round
+    (ratio 1) of random gang snapshots and of config #4's shape, both N32 and
+    64-bit first-fit sums (caps >= 2^26 in seed 3)."""
+    monkeypatch.setenv("KP_ACC_BIG_RATIO", "1")
+    if seed == 2:
+        w = synth.config4(20_000, 2_000)
+        p = _abi.default_params(**synth.CONFIG_PARAMS[4])
+    else:
+        w = random_workload(500 + seed, J=4000, N=300, max_gang=8)
+        if seed == 3:
+            w = synth.Workload(w.J, w.N, w.D, w.req * (1 << 22), w.cap * (1 << 22), w.used * (1 << 22),
+                               w.prio, w.gang_id, w.gang_size, w.topo, name="rand_big_caps")
+        p = _abi.default_params(score_mode=seed % 2, n_cand=[16, 8, 16, 32][seed])
+    with Placer(device=0) as pl:
+        g = pl.place(w, p)
+        g2 = pl.place(w, p)
+    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
+    _assert_same(g, o, f"accept long-row form seed {seed}")
+    _assert_same(g2, o, f"accept long-row form seed {seed}, second solve")
+
+
 def test_pass_wg_random_parity(oracle, monkeypatch):
     """The one-workgroup loop on random snapshots: gangs spread over several
     nodes, both score modes, D <= 4, 32-candidate lists (32-lane groups)."""
