@@ -54,6 +54,19 @@ def test_config3_full_sharded_in_process(oracle, shards):
     assert st["rounds"] == o["rounds"] and st["passes"] == o["passes"]
 
 
+@pytest.mark.parametrize("follow", ["0", "1"])
+def test_config3_full_sharded_pass_follow(oracle, monkeypatch, follow):
+    """The sharded solve with host-followed passes off (every round enqueues
+    max_passes) and at M = 1 (each shard's host waits for every pass flag
+    before enqueueing the next pass): 4 worker threads, each following its own
+    replicated passes after the round's exchange; same placement and counts."""
+    monkeypatch.setenv("KP_PASS_FOLLOW", follow)
+    w, p, o = _config3_full(oracle)
+    with Placer(gpu_ids=[0] * 4) as pl:
+        g = pl.place(w, p)
+    _assert_same(g, o, f"config3 full, 4 shards, follow {follow}")
+
+
 def test_create_multi_distinct_ids_beyond_the_box():
     """Distinct GPU ids take the RCCL form (ncclCommInitAll). On a box with
     fewer GPUs than ids the context must fail cleanly with KP_ENODEV, not
