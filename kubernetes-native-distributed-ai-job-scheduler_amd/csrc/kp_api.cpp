@@ -131,29 +131,7 @@ static int ensure_nodes(kp_ctx *c, int32_t N, int32_t D) {
   KP_TRY(dalloc(&c->d.nrec, (size_t)n + 16));
   KP_TRY(dalloc(&c->d.nst, (size_t)n * 16));
   KP_TRY(dalloc(&c->d.perm, (size_t)n));
-  KP_TRY(dalloc(&c->d.npos, (size_t)n));
-  KP_TRY(dalloc(&c->d.clist, (size_t)2 * n));
-  KP_TRY(dalloc(&c->d.chg, (size_t)n));
-  // usage-change stamps: round serials start at 0
-  KP_HIP(hipMemsetAsync(c->d.chg, 0xFF, sizeof(int32_t) * (size_t)n, c->stream));
   c->cap_N = n;
-  return KP_OK;
-}
-
-// per-unit lists of the incremental candidate phase (kp_incr.hip) and the
-// per-round rescan rows
-static int ensure_incr(kp_ctx *c, int32_t U, int32_t KL) {
-  if (c->d.ukey && U <= c->cap_incr_U && KL <= c->cap_incr_KL) return KP_OK;
-  c->cap_incr_U = 0;
-  const size_t u = (size_t)std::max(U, 64);
-  KP_TRY(dalloc(&c->d.ukey, u * KL));
-  KP_TRY(dalloc(&c->d.unode, u * KL));
-  KP_TRY(dalloc(&c->d.ucnt, u));
-  KP_TRY(dalloc(&c->d.ubound, u));
-  KP_TRY(dalloc(&c->d.rs_slot, u));
-  KP_TRY(dalloc(&c->d.rs_unit, u));
-  c->cap_incr_U = (int32_t)u;
-  c->cap_incr_KL = KL;
   return KP_OK;
 }
 
@@ -212,7 +190,6 @@ static int ensure_units(kp_ctx *c, int32_t U, int32_t J) {
     KP_TRY(dalloc(&c->d.csr_keys, pm));
     KP_TRY(dalloc(&c->d.csr_vals, pm));
     KP_TRY(dalloc(&c->d.pass_flag, kPassFlagWords));
-    KP_TRY(dalloc(&c->d.sdone, u));
     KP_TRY(dalloc(&c->d.counters, 64));
     KP_TRY(dalloc(&c->d.stats, 1));
     c->d.temp_bytes = rocprim_temp_bytes((int32_t)std::min<size_t>(pm, INT32_MAX));
@@ -356,17 +333,10 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = knob("KP_SCORE_NPL")) c->score_npl = std::atoi(e) == 4 ? 4 : 2;
   if (const char *e = knob("KP_COMPACT_MAX")) c->compact_max = std::atoi(e);
   if (const char *e = knob("KP_FUSED")) c->fused_enabled = std::atoi(e) != 0;
-  if (const char *e = knob("KP_INCR")) c->incr_enabled = std::atoi(e) != 0;
-  if (const char *e = knob("KP_INCR_CTHR_DIV")) c->incr_cthr_div = std::max(1, std::atoi(e));
-  if (const char *e = knob("KP_INCR_TRACE")) c->incr_trace = std::atoi(e) != 0;
   if (const char *e = knob("KP_PREEMPT32")) c->preempt32 = std::atoi(e) != 0;
   if (const char *e = knob("KP_ACC_LIST")) c->acc_list = std::atoi(e);
-  if (const char *e = knob("KP_PASS_LOOP")) c->pass_loop_enabled = std::atoi(e) != 0;
-  if (const char *e = knob("KP_PASS_WG_T")) c->pass_wg_max = std::max(0, std::atoi(e));
   if (const char *e = knob("KP_ACC_BIG_RATIO")) c->acc_big_ratio = std::max(0, std::atoi(e));
   if (const char *e = knob("KP_PASS_FOLLOW")) c->pass_follow = std::max(0, std::min(64, std::atoi(e)));
-  if (const char *e = knob("KP_PASS_LOOP_FORM")) c->pass_loop_form = std::atoi(e) == 1 ? 1 : 2;
-  if (const char *e = knob("KP_PASS_LOOP_PMAX")) c->pass_loop_pmax = std::max(1, std::min(256, std::atoi(e)));
   if (const char *e = knob("KP_KEYS_MERGE")) c->keys_merge_enabled = std::atoi(e) != 0;
   if (const char *e = knob("KP_ROUND_BEGIN")) c->round_begin = std::atoi(e) != 0;
   if (const char *e = knob("KP_CSR_SORT")) c->csr_count_enabled = std::atoi(e) == 0;
@@ -518,21 +488,12 @@ static int load_nodes_impl(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap,
                           hipMemcpyHostToDevice, c->stream));
     KP_HIP(hipMemcpyAsync(c->d.perm, c->h_perm.data(), sizeof(int32_t) * N,
                           hipMemcpyHostToDevice, c->stream));
-    std::vector<int32_t> npos;
-    try {
-      npos.resize(N);
-    } catch (const std::bad_alloc &) {
-      return fail(KP_ENOMEM, "kp_load_nodes: host copy");
-    }
-    for (int32_t i = 0; i < N; ++i) npos[(size_t)c->h_perm[i]] = i;
-    KP_HIP(hipMemcpyAsync(c->d.npos, npos.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice,
-                          c->stream));
-    KP_HIP(hipStreamSynchronize(c->stream));  // npos is a local
   }
   // the victim pool belongs to the previous node table
   KP_HIP(hipMemsetAsync(c->d.roff, 0, sizeof(int32_t) * ((size_t)N + 1), c->stream));
   KP_HIP(hipStreamSynchronize(c->stream));
   c->R = 0;
+  c->pre_key_ok = false;  // described the previous table's victim pool
   c->N = N;
   c->D = D;
   c->max_cap = 0;
@@ -797,7 +758,6 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
       if (!ptr) return fail(KP_ENOMEM, "kp_solve: a device buffer is missing");
   }
   KP_TRY(launch_reset_units(c, p->tie_seed));  // also the salts of the rotated tie-break
-  loop_profile_reset();  // KP_LOOP_PROFILE builds only
   c->pack_sp = sp;
   c->pack_canonical = true;  // the solve scores in canonical column order
   const int32_t shard = c->u_hi - c->u_lo;
@@ -819,32 +779,12 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   c->pack_fused = fused;
   c->pack_full = true;
   c->last_fused = fused;
-  // Incremental candidate phase (kp_incr.hip): the first round scans in full
-  // and keeps every unit's top-KL list (KL >= K, the merge holds <= 2,048
-  // keys per row); later rounds re-score only the nodes the previous round
-  // changed. Needs the one-launch round start (it compacts the changed nodes).
-  const int32_t ntiles = std::max(c->fz_P / 1024, 1);
-  const bool incr = fused && c->incr_enabled && c->round_begin && shard > 0 &&
-                    shard <= c->compact_max;
-  const int32_t KL = incr ? std::min<int32_t>(KP_MAX_CAND, std::max<int32_t>(K, 2048 / ntiles)) : K;
-  c->incr_active = incr;
-  struct IncrOff {  // the flag never outlives the solve (the accept kernels read it)
-    kp_ctx *c;
-    ~IncrOff() { c->incr_active = false; }
-  } incr_off{c};
-  ScoreParams sp_list = sp;
-  sp_list.n_cand = KL;
   int64_t rpc = rows_per_chunk(c);
   if (fused) {
     rpc = INT64_MAX;  // no matrix, no chunks: per row only tiles x K keys
-    KP_TRY(ensure_part(c, (int64_t)std::max(shard, 1) * (c->fz_P / 1024) * KL));
+    KP_TRY(ensure_part(c, (int64_t)std::max(shard, 1) * (c->fz_P / 1024) * K));
     if (!c->d.part || !c->d.colnode || !c->d.wshift)
       return fail(KP_ENOMEM, "kp_solve: a fused-path buffer is missing");
-    if (incr) {
-      KP_TRY(ensure_incr(c, U, KL));
-      if (!c->d.ukey || !c->d.chg || !c->d.clist || !c->d.npos)
-        return fail(KP_ENOMEM, "kp_solve: an incremental-phase buffer is missing");
-    }
   } else {
     KP_TRY(ensure_matrix(c, (int32_t)std::min<int64_t>(std::max(shard, 1), rpc)));
   }
@@ -863,33 +803,13 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   KP_TRY(E.make(&t1, hipEventDefault));
   KP_HIP(hipMemsetAsync(c->d.stats, 0, sizeof(SolveStats), c->stream));
   KP_HIP(hipMemsetAsync(c->d.pass_flag, 0, sizeof(int32_t) * kPassFlagWords, c->stream));
-  // changed-node and rescan counters of both round parities
-  KP_HIP(hipMemsetAsync(c->d.counters + kCCount, 0, sizeof(int32_t) * 4, c->stream));
   KP_HIP(hipEventRecord(t0, c->stream));
   std::vector<int32_t> round_active;  // exact active units per round (when known)
   kp_timing tm{};
   // filter+score and top-K select of `rows` rows starting at act_local[r0];
   // rows_dev (nullable) clamps them to the device count
-  const ListOut lo_none{nullptr, nullptr, nullptr, nullptr, nullptr, K};
-  const ListOut lo_full{c->d.ukey, c->d.unode, c->d.ucnt, c->d.ubound, nullptr, K};
-  const ListOut lo_rescan{c->d.ukey, c->d.unode, c->d.ucnt, c->d.ubound, c->d.rs_slot, K};
   auto score_select = [&](int64_t r0, int32_t rows, const int32_t *rows_dev,
                           int32_t round) -> int {
-    if (incr && round > 0) {
-      // incremental round: the lists absorb the changed nodes; the rows they
-      // cannot answer are rescanned (k_score_topk + merge over the round's
-      // rescan list, device count; not bracketed by the profiling events)
-      c->keys_in_merge = false;
-      if (c->world == 1 && c->keys_merge_enabled && rows > 0) {
-        KP_TRY(csr_prepare(c, rows, K));
-        c->keys_in_merge = c->csr_mode == 1;
-      }
-      KP_TRY(launch_cand_update(c, sp, KL, rows, rows_dev, round, c->keys_in_merge));
-      KP_TRY(launch_score_topk(c, sp_list, c->d.rs_unit, rows, ksh, c->d.cand_local,
-                               c->d.counters + kRsCount + (round & 1), lo_rescan, false));
-      tm.incr_rounds++;
-      return KP_OK;
-    }
     // profiling brackets the filter+score launch only (each event record is
     // a GPU packet of a few us: the select is timed by rocprofv3 instead)
     KEv ke{nullptr, nullptr, round, rows};
@@ -910,9 +830,8 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
       }
       // the profiling bracket ends right after k_score_topk (before the merge)
       c->fz_end_event = c->profiling ? ke.b : nullptr;
-      const int rc = launch_score_topk(c, incr ? sp_list : sp, c->d.act_local + r0, rows, ksh,
-                                       c->d.cand_local + r0 * K, rows_dev,
-                                       incr ? lo_full : lo_none, true);
+      const int rc = launch_score_topk(c, sp, c->d.act_local + r0, rows, ksh,
+                                       c->d.cand_local + r0 * K, rows_dev, true);
       c->fz_end_event = nullptr;
       KP_TRY(rc);
     } else {
@@ -930,17 +849,24 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     return KP_OK;
   };
   double pass_wait_us = 0;
+  hipEvent_t evP;  // host-followed passes: the fallback wait on the stream
+  KP_TRY(E.make(&evP, hipEventDisableTiming));
+  // this round's serial: the host-followed pass tags (hpass) keep 30 bits of
+  // it, so before it reaches 2^30 the slots are reset (once the stream has
+  // drained, no k_accept still writes them) and the serial restarts: a stale
+  // slot can never match
+  auto next_serial = [&]() -> int {
+    if (c->round_serial >= (1 << 30) - 1) {
+      KP_TRY(wait_stream(c, evP));
+      for (int i = 0; i < 64; ++i) c->hpass[i] = -1;
+      c->round_serial = 0;
+    }
+    c->cur_serial = c->round_serial++;
+    return KP_OK;
+  };
   auto passes_of_round = [&](int32_t A, const int32_t *A_dev, bool follow) -> int {
     // also opens the slots, banks + clears the pass flags
     KP_TRY(launch_csr_build(c, A, K, A_dev));
-    // small rounds: every pass in one persistent launch
-    bool looped = false;
-    KP_TRY(launch_pass_wg(c, sp, A, A_dev, p->max_passes, &looped));
-    if (!looped) KP_TRY(launch_pass_loop(c, sp, A, A_dev, p->max_passes, &looped));
-    if (looped) {
-      tm.loop_rounds++;
-      return KP_OK;
-    }
     // passes run back to back on the device: no host round trip inside a round
     const int32_t M = follow && A > 0 && c->N > 0 ? c->pass_follow : 0;
     if (M == 0 || M >= p->max_passes) {
@@ -967,9 +893,17 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
         const int32_t *f = c->hpass + (pass - M);
         int32_t v;
         for (uint32_t spin = 0; ((v = __atomic_load_n(f, __ATOMIC_ACQUIRE)) & ~1) != tag; ++spin) {
+          // a kp_create_multi shard whose peer failed before its exchange:
+          // this round's collective never completes, so its pass flags never
+          // arrive (the multi context aborts the communicators afterwards)
+          if ((spin & 255u) == 255u && c->peer_failed &&
+              c->peer_failed->load(std::memory_order_acquire))
+            return fail(KP_ERCCL, "kp_solve: a peer shard failed; the exchange cannot complete");
           if ((spin & 1023u) == 1023u &&
               std::chrono::steady_clock::now() - w0 > std::chrono::milliseconds(200)) {
-            KP_HIP(hipStreamSynchronize(c->stream));  // the stream has stored it for sure
+            // the stream has stored it for sure once it drains (polled, so a
+            // failed peer still releases a multi shard)
+            KP_TRY(wait_stream(c, evP));
             v = __atomic_load_n(f, __ATOMIC_ACQUIRE);
             if ((v & ~1) != tag) return fail(KP_EHIP, "kp_solve: pass flag not delivered");
             break;
@@ -1028,8 +962,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     };
     for (int32_t r = 0; A_bound > 0; ++r) {
       if (p->max_rounds > 0 && r >= p->max_rounds) break;
-      c->incr_round = r;
-      c->cur_serial = c->round_serial++;
+      KP_TRY(next_serial());
       bool direct = true;
       KP_TRY(launch_active_async(c, c->u_lo, c->u_hi, A_h, &direct));
       if (!direct) KP_HIP(hipEventRecord(evA, c->stream));
@@ -1047,16 +980,6 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
       const int32_t *A_dev = c->d.counters;
       KP_TRY(score_select(0, (int32_t)A_bound, A_dev, r));
       KP_TRY(passes_of_round((int32_t)A_bound, A_dev, true));
-      if (c->incr_trace && incr) {  // diagnostics: synchronous per-round counters
-        int32_t h[4] = {0, 0, 0, 0};
-        KP_HIP(hipMemcpyAsync(h, c->d.counters, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-        KP_HIP(hipMemcpyAsync(h + 1, c->d.counters + kCCount + (r & 1), sizeof(int32_t),
-                              hipMemcpyDeviceToHost, c->stream));
-        KP_HIP(hipMemcpyAsync(h + 2, c->d.counters + kRsCount + (r & 1), sizeof(int32_t),
-                              hipMemcpyDeviceToHost, c->stream));
-        KP_HIP(hipStreamSynchronize(c->stream));
-        std::fprintf(stderr, "kp_incr round %d active %d changed %d rescanned %d\n", r, h[0], h[1], h[2]);
-      }
       KP_TRY(round_count(direct));  // landed long ago on a busy round
       round_active.push_back(*A_h);
       A_bound = *A_h;
@@ -1090,8 +1013,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     int64_t G_bound = U;
     for (int32_t r = 0; G_bound > 0; ++r) {
       if (p->max_rounds > 0 && r >= p->max_rounds) break;
-      c->incr_round = r;
-      c->cur_serial = c->round_serial++;
+      KP_TRY(next_serial());
       const int32_t B = (int32_t)std::min<int64_t>(Smax, G_bound);  // per-rank slot bound
       if (shard > 0) {
         KP_TRY(launch_active_async(c, c->u_lo, c->u_hi, Al_h));
@@ -1135,10 +1057,6 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
                           c->stream));
   SolveStats dst{};
   KP_HIP(hipMemcpyAsync(&dst, c->d.stats, sizeof dst, hipMemcpyDeviceToHost, c->stream));
-  int32_t *loop_err = c->pinned + 384;
-  *loop_err = 0;
-  KP_HIP(hipMemcpyAsync(loop_err, c->d.pass_flag + kLoopErr, sizeof(int32_t), hipMemcpyDeviceToHost,
-                        c->stream));
   if (c->world > 1) {
     hipEvent_t evF;
     KP_TRY(E.make(&evF, hipEventDisableTiming));
@@ -1147,7 +1065,6 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     KP_HIP(hipStreamSynchronize(c->stream));
   }
   c->in_collective = false;  // every collective of this solve completed
-  if (*loop_err) return fail(KP_EHIP, "kp_solve: a pass-loop grid barrier timed out");
   const int32_t rounds = (int32_t)dst.rounds, passes = (int32_t)dst.passes;
   const int64_t pairs = dst.active_sum * N;
   tm.solve_ms = ev_ms(t0, t1);
@@ -1319,7 +1236,6 @@ void kp_destroy(kp_ctx *c) {
   }
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  loop_profile_dump();  // KP_LOOP_PROFILE builds only: the last solve's pass-loop phases
   if (c->nccl_comm) ncclCommDestroy(static_cast<ncclComm_t>(c->nccl_comm));
   DevState &d = c->d;
   if (d.fz_prof) {  // KP_FZ_PROF: the accumulated phase clocks
@@ -1360,7 +1276,7 @@ void kp_destroy(kp_ctx *c) {
                   d.inv, d.ent_unit,
                   d.ent_slot, d.ent_size, d.ent_lead, d.ent_q, d.perm,
                   d.csr_kin, d.csr_vin,
-                  d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.sdone, d.counters,
+                  d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
                   d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.roff,
                   d.rreq, d.rsuf, d.rprio, d.pre_node, d.pre_vict, d.pre_cost,
                   d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.nrec, d.nst, d.stats, d.np32, d.colnode, d.wshift, d.part, d.fz_prof,

@@ -452,8 +452,7 @@ __device__ __forceinline__ int mbcnt64(uint64_t m) {
 }
 
 // k_csr_keys' per-round state reset, thread t of the extra workgroups of the
-// kernel that opens the round's slots (the candidate merge or the incremental
-// candidate update, rk.enabled): round statistics, the previous round's
+// kernel that opens the round's slots (the candidate merge, rk.enabled): round statistics, the previous round's
 // productive passes, node segments / flags, window flags
 __device__ __forceinline__ void round_keys_init(const RoundKeys &rk, int64_t t) {
   if (t == 0) {
@@ -473,7 +472,6 @@ __device__ __forceinline__ void round_keys_init(const RoundKeys &rk, int64_t t) 
     if (rk.pass_flag[t] != 0)
       atomicAdd(reinterpret_cast<unsigned long long *>(&rk.st->passes), 1ull);
     rk.pass_flag[t] = 0;
-    if (t == 0) rk.pass_flag[kLoopBar] = 0;  // the pass loop's barrier counter
   }
 }
 

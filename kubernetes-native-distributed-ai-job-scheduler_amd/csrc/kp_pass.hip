@@ -135,57 +135,6 @@ struct PassProf {
 
 constexpr uint32_t kNoBid = 0xFFFFFFFFu;  // tag that matches no pass
 
-// ---- coherent accessors of the persistent pass loop (k_pass_loop) -------------
-// Inside one launch, workgroups on different XCDs exchange the pass state
-// (bids, flags, usage) between grid barriers. With COH every such word is
-// stored write-through and loaded past the L1 (agent-scope relaxed atomics:
-// `global_store/load ... sc1`, 4- or 8-byte), the hand-off form of the gfx950
-// visibility rules (MI355X_MICROARCH.md § visibility, first row); usage is
-// updated by agent-scope atomic adds. Without COH (one pass per launch) they
-// are plain accesses: the kernel boundary publishes them.
-#ifndef KP_LOOP_TIMING_LD
-#define KP_LOOP_TIMING_LD 1  // timing experiments only: 0 = plain loads (incoherent)
-#endif
-#ifndef KP_LOOP_TIMING_ST
-#define KP_LOOP_TIMING_ST 1  // timing experiments only: 0 = plain stores (incoherent)
-#endif
-template <bool COH, typename T>
-__device__ __forceinline__ T ldc(const T *p) {
-  if constexpr (COH && KP_LOOP_TIMING_LD)
-    return __hip_atomic_load(const_cast<T *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else
-    return *p;
-}
-template <bool COH, typename T>
-__device__ __forceinline__ void stc(T *p, T v) {
-  if constexpr (COH && KP_LOOP_TIMING_ST)
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else
-    *p = v;
-}
-// 16-byte gang part records as two 8-byte halves
-template <bool COH>
-__device__ __forceinline__ int4 ldc4(const int4 *p) {
-  if constexpr (COH) {
-    const uint64_t *q = reinterpret_cast<const uint64_t *>(p);
-    const uint64_t lo = ldc<true>(q), hi = ldc<true>(q + 1);
-    return make_int4((int32_t)(uint32_t)lo, (int32_t)(uint32_t)(lo >> 32), (int32_t)(uint32_t)hi,
-                     (int32_t)(uint32_t)(hi >> 32));
-  } else {
-    return *p;
-  }
-}
-template <bool COH>
-__device__ __forceinline__ void stc4(int4 *p, int4 v) {
-  if constexpr (COH) {
-    uint64_t *q = reinterpret_cast<uint64_t *>(p);
-    stc<true>(q, (uint64_t)(uint32_t)v.x | ((uint64_t)(uint32_t)v.y << 32));
-    stc<true>(q + 1, (uint64_t)(uint32_t)v.z | ((uint64_t)(uint32_t)v.w << 32));
-  } else {
-    *p = v;
-  }
-}
-
 // ---- inverse index (once per round) --------------------------------------------
 // Also re-initialises the round's pass state (bids, window flags, node
 // segments, pass flags) so no memset launch is needed, and opens the round's
@@ -232,7 +181,6 @@ __global__ void k_csr_keys(int32_t A, int32_t K, int32_t N, int64_t nwin,
     if (pass_flag[t] != 0) atomicAdd(reinterpret_cast<unsigned long long *>(&st->passes), 1ull);
     pass_flag[t] = 0;
   }
-  if (t == 0) pass_flag[kLoopBar] = 0;  // the pass loop's barrier counter
 }
 
 __global__ void k_csr_finish(int32_t P, int32_t N, int32_t K, int32_t D, int32_t U,
@@ -474,7 +422,6 @@ struct PlanArgs {
   const int64_t *ent_q;
   int64_t *winmin;
   uint32_t key_off;        // W32 member loop: 64 * w_spread + 1 (plan_key_ok)
-  int32_t *sdone;          // k_pass_loop: [slot] placed by an accept of this round
   uint64_t *pp;            // KP_PASS_PROFILE only
   const SolveStats *st;    // KP_PASS_PROFILE only (round index)
 };
@@ -482,7 +429,7 @@ struct PlanArgs {
 // the slots of wave `wave_global` (whole wave). The slot loads do not wait
 // for the device slot count: they are issued together with it (slots past the
 // count but below the host bound are readable and ignored).
-template <int D, int G, bool W32, bool COH = false>
+template <int D, int G, bool W32>
 __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int wave_global) {
   constexpr int SPW = 64 / G;  // slots per wave
   constexpr uint64_t GMASK = G == 64 ? ~0ull : ((1ull << G) - 1);
@@ -500,17 +447,13 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
   const int32_t u0 = pa.act[aa];
   const int32_t node = gl < K ? pa.cand[(int64_t)aa * K + gl] : -1;
   const int32_t e_inv = gl < K ? pa.inv[(int64_t)aa * K + gl] : 0;  // valid iff node >= 0
-  // k_pass_loop: a slot placed by an earlier pass's accept (another
-  // workgroup) is closed; pass 0 clears the word before the first barrier
-  const int32_t done = COH && pass > 0 ? ldc<true>(&pa.sdone[aa]) : 0;
-  const int32_t prev = !COH && pass > 0 ? pa.pass_flag[pass - 1] : 1;
+  const int32_t prev = pass > 0 ? pa.pass_flag[pass - 1] : 1;
   const int32_t A = pa.A_dev ? min(pa.A, *pa.A_dev) : pa.A;
   // a pass after one without proposals has none either (usage unchanged,
   // open slots only close): the round is over
   if (!prev) return;
   const bool in = a < A;
-  if (COH && pass == 0 && in && gl == 0) stc<true>(&pa.sdone[a], 0);
-  const bool slot_ok = in && op && !done;
+  const bool slot_ok = in && op;
   KP_PP_MARK(0);
   if (__ballot(slot_ok) == 0) return;
   KP_PP_WORK();
@@ -559,7 +502,7 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       q32[d] = (uint32_t)qq[d];
-      const uint32_t uu = (uint32_t)ldc<COH>(&pa.used[(int64_t)d * N + nn]);
+      const uint32_t uu = (uint32_t)pa.used[(int64_t)d * N + nn];
       const uint32_t cc = REC ? ncap[d] : (uint32_t)pa.cap[(int64_t)d * N + nn];
       const uint32_t rr = REC ? nR[d] : pa.R32[(int64_t)d * N + nn];
       const uint32_t kk = REC ? nK[d] : pa.K32[(int64_t)d * N + nn];
@@ -636,7 +579,7 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       c_[d] = pa.cap[(int64_t)d * N + nn];
-      u0_[d] = ldc<COH>(&pa.used[(int64_t)d * N + nn]);
+      u0_[d] = pa.used[(int64_t)d * N + nn];
     }
     for (int m = 0; m < szmax; ++m) {
       const bool live = !fail && m < sz;  // group-uniform
@@ -669,30 +612,27 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
   if (!slot_ok) return;
   if (fail) {
     if (gl == 0) {
-      if (COH)  // the slot's own word (open[] stays as loaded for the whole launch)
-        stc<true>(&pa.sdone[a], 1);
-      else
-        pa.open[a] = 0;
+      pa.open[a] = 0;
       if (pass == 0) pa.status[u] = kNoFit;
     }
     return;
   }
   if (prop) {
     // bid tag: pass << 16 | parts << 8 | members (parts <= K <= 32, members <= 64)
-    stc<COH>(&pa.bid[e_inv], ((uint32_t)pass << 16) | ((uint32_t)np << 8) | (uint32_t)planned);
-    stc<COH>(&pa.s0_out[e_inv], s0);
-    stc<COH>(&pa.win[e_inv >> 6], pass);
-    stc<COH>(&pa.node_flag[node], pass);
+    pa.bid[e_inv] = ((uint32_t)pass << 16) | ((uint32_t)np << 8) | (uint32_t)planned;
+    pa.s0_out[e_inv] = s0;
+    pa.win[e_inv >> 6] = pass;
+    pa.node_flag[node] = pass;
     if (np > 1) {
       const int idx = __popcll(pm & ((1ull << gl) - 1));
-      stc4<COH>(&pa.gpart[(int64_t)a * K + idx], make_int4(node, planned, inc - planned, s0));
+      pa.gpart[(int64_t)a * K + idx] = make_int4(node, planned, inc - planned, s0);
     }
   }
   if (gl == 0) {
-    stc<COH>(&pa.pass_flag[pass], 1);
+    pa.pass_flag[pass] = 1;
     if (np > 1) {
       pa.nparts[a] = np;
-      stc<COH>(&pa.arrive[a], 0);
+      pa.arrive[a] = 0;
     }
   }
 }
@@ -746,7 +686,7 @@ struct Win {
   NT need[D];
 };
 
-template <int D, bool N32, bool COH = false>
+template <int D, bool N32>
 __device__ __forceinline__ void load_win(Win<D, N32> &w, int wi, int lane, int32_t e0, int32_t e1,
                                          int32_t pass, int64_t P,
                                          const uint32_t *__restrict__ bid,
@@ -761,12 +701,12 @@ __device__ __forceinline__ void load_win(Win<D, N32> &w, int wi, int lane, int32
   w.np = 0;
   const bool in_row = wi >= 0 && w.e >= e0 && w.e < e1;
   const int32_t ee = in_row ? w.e : e0;
-  const uint32_t t = ldc<COH>(&bid[ee]);
+  const uint32_t t = bid[ee];
   w.unit = ent_unit[ee];
   w.size = ent_size[ee];
   w.lead = ent_lead[ee];
   w.slot = ent_slot[ee];
-  w.s0 = ldc<COH>(&s0[ee]);
+  w.s0 = s0[ee];
   int64_t qd[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) qd[d] = ent_q[(int64_t)d * P + ee];
@@ -789,11 +729,6 @@ struct AcceptOut {
   int64_t *used;
   uint8_t *open;
   int32_t *status, *job_node, *job_score;
-  int32_t *sdone;  // k_pass_loop: a placed slot is closed here instead of open[]
-  // incremental candidate phase: chg[node] = serial for every node whose
-  // usage this round changes (a plain store, nothing waits on it)
-  int32_t *chg;
-  int32_t serial;
 };
 
 // all-or-nothing commit of a multi-node gang by the wave that accepted its
@@ -805,31 +740,20 @@ constexpr int kGangPreN = kGangPre > 0 ? kGangPre : 1;
 template <int D>
 __device__ __forceinline__ void commit_part(const AcceptOut &o, int32_t lead, const int4 &g,
                                             const int64_t (&qq)[D]) {
-  bool any = false;
 #pragma unroll
   for (int d = 0; d < D; ++d)
-    if (qq[d] != 0) {
+    if (qq[d] != 0)
       atomicAdd(reinterpret_cast<unsigned long long *>(&o.used[(int64_t)d * o.N + g.x]),
                 (unsigned long long)((int64_t)g.y * qq[d]));
-      any = true;
-    }
-  if (any && o.chg) o.chg[g.x] = o.serial;
   for (int m = 0; m < g.y; ++m) {
     o.job_node[lead + g.z + m] = g.x;
     o.job_score[lead + g.z + m] = g.w;
   }
 }
 
-// a placed slot closes: open[] (one pass per launch) or sdone[] (k_pass_loop)
-template <bool COH>
-__device__ __forceinline__ void close_slot(const AcceptOut &o, int32_t slot) {
-  if (COH)
-    stc<true>(&o.sdone[slot], 1);
-  else
-    o.open[slot] = 0;
-}
+__device__ __forceinline__ void close_slot(const AcceptOut &o, int32_t slot) { o.open[slot] = 0; }
 
-template <int D, bool COH = false>
+template <int D>
 __device__ __forceinline__ void commit_gang(const AcceptOut &o, int32_t slot, int32_t unit,
                                          int32_t lead, int32_t np, const int4 (&pre)[kGangPreN],
                                          const int64_t (&qq)[D]) {
@@ -837,9 +761,9 @@ __device__ __forceinline__ void commit_gang(const AcceptOut &o, int32_t slot, in
   for (int i = 0; i < kGangPre; ++i)  // static indices: the parts stay in registers
     if (i < np) commit_part<D>(o, lead, pre[i], qq);
   for (int i = kGangPre; i < np; ++i)
-    commit_part<D>(o, lead, ldc4<COH>(&o.gpart[(int64_t)slot * o.K + i]), qq);
+    commit_part<D>(o, lead, o.gpart[(int64_t)slot * o.K + i], qq);
   o.status[unit] = kPlaced;
-  close_slot<COH>(o, slot);
+  close_slot(o, slot);
 }
 
 template <bool N32>
@@ -857,7 +781,7 @@ __device__ __forceinline__ int64_t readlane_nt(int64_t v, int l) { return readla
 
 // Exact parallel first-fit of one 64-entry window against the node's
 // remaining capacity `rem` (wave-uniform), in lane (= rank) order.
-template <int D, bool N32, bool COH = false>
+template <int D, bool N32>
 __device__ __forceinline__ void decide_window(const Win<D, N32> &wc,
                                               typename Win<D, N32>::NT (&rem)[D],
                                               typename Win<D, N32>::NT (&add)[D], int lane,
@@ -899,7 +823,7 @@ __device__ __forceinline__ void decide_window(const Win<D, N32> &wc,
         o.job_score[wc.lead + i] = wc.s0;
       }
       o.status[wc.unit] = kPlaced;
-      close_slot<COH>(o, wc.slot);
+      close_slot(o, wc.slot);
 #pragma unroll
       for (int d = 0; d < D; ++d) add[d] += wc.need[d];
     } else {  // one part of a multi-node gang: the part count came with the bid
@@ -908,7 +832,7 @@ __device__ __forceinline__ void decide_window(const Win<D, N32> &wc,
       int4 pre[kGangPreN];
 #pragma unroll
       for (int i = 0; i < kGangPre; ++i)
-        pre[i] = i < wc.np ? ldc4<COH>(&o.gpart[(int64_t)wc.slot * o.K + i]) : make_int4(0, 0, 0, 0);
+        pre[i] = i < wc.np ? o.gpart[(int64_t)wc.slot * o.K + i] : make_int4(0, 0, 0, 0);
       int64_t qq[D];
 #pragma unroll
       for (int d = 0; d < D; ++d) qq[d] = o.q[(int64_t)d * o.U + wc.unit];
@@ -918,16 +842,16 @@ __device__ __forceinline__ void decide_window(const Win<D, N32> &wc,
         int4 post[KP_GANG_POST];
 #pragma unroll
         for (int i = 0; i < KP_GANG_POST; ++i)
-          post[i] = i < wc.np ? ldc4<COH>(&o.gpart[(int64_t)wc.slot * o.K + i]) : make_int4(0, 0, 0, 0);
+          post[i] = i < wc.np ? o.gpart[(int64_t)wc.slot * o.K + i] : make_int4(0, 0, 0, 0);
 #pragma unroll
         for (int i = 0; i < KP_GANG_POST; ++i)
           if (i < wc.np) commit_part<D>(o, wc.lead, post[i], qq);
         for (int i = KP_GANG_POST; i < wc.np; ++i)
-          commit_part<D>(o, wc.lead, ldc4<COH>(&o.gpart[(int64_t)wc.slot * o.K + i]), qq);
+          commit_part<D>(o, wc.lead, o.gpart[(int64_t)wc.slot * o.K + i], qq);
         o.status[wc.unit] = kPlaced;
-        close_slot<COH>(o, wc.slot);
+        close_slot(o, wc.slot);
 #else
-        commit_gang<D, COH>(o, wc.slot, wc.unit, wc.lead, wc.np, pre, qq);
+        commit_gang<D>(o, wc.slot, wc.unit, wc.lead, wc.np, pre, qq);
 #endif
       }
     }
@@ -962,7 +886,7 @@ struct AccArgs {
 // flagged windows whose smallest request no longer fits the node's remaining
 // capacity in some dim are skipped unread (a contested node fills after a
 // few windows; the rest of its long bidder row is then rejected unread).
-template <int D, bool N32, bool COH = false, int B = KP_ACC_BATCH>
+template <int D, bool N32, int B = KP_ACC_BATCH>
 __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int node, int32_t e0,
                                             int32_t e1) {
   using NT = typename Win<D, N32>::NT;
@@ -973,11 +897,11 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
   KP_PP_DECL(ac.pp, 16, ac.pp ? (int)(ac.st->rounds - 1) * 16 + pass : 1024);
 #endif
   if (e0 < 0) return;  // no bidder row this round
-  const int32_t nf = ldc<COH>(&ac.node_flag[node]);
+  const int32_t nf = ac.node_flag[node];
   NT rem[D], add[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    rem[d] = (NT)(ac.cap[(int64_t)d * N + node] - ldc<COH>(&o.used[(int64_t)d * N + node]));
+    rem[d] = (NT)(ac.cap[(int64_t)d * N + node] - o.used[(int64_t)d * N + node]);
     add[d] = 0;
   }
   const int32_t w0 = e0 >> 6, w1 = (e1 - 1) >> 6;
@@ -986,12 +910,12 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
 #endif
   if (KP_ACC_FAST1 && w0 == w1) {
     Win<D, N32> wv;
-    load_win<D, N32, COH>(wv, w0, lane, e0, e1, pass, ac.P, ac.bid, ac.ent_q, ac.ent_unit,
+    load_win<D, N32>(wv, w0, lane, e0, e1, pass, ac.P, ac.bid, ac.ent_q, ac.ent_unit,
                           ac.ent_size, ac.ent_lead, ac.ent_slot, ac.s0);
     KP_PP_MARK(0);
     if (nf != pass) return;  // nobody bid on this node in this pass
     KP_PP_WORK();
-    decide_window<D, N32, COH>(wv, rem, add, lane, node, o);
+    decide_window<D, N32>(wv, rem, add, lane, node, o);
     KP_PP_MARK(3);
   } else {
     constexpr int BATCH = B;  // flagged windows whose operands are loaded together
@@ -1000,8 +924,8 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
       const bool mine = wi <= w1;
       int64_t wmin[D];
 #pragma unroll
-      for (int d = 0; d < D; ++d) wmin[d] = mine ? ldc<COH>(&ac.winmin[(int64_t)d * ac.nwin + wi]) : 0;
-      const int32_t wf = mine ? ldc<COH>(&ac.win[wi]) : -1;
+      for (int d = 0; d < D; ++d) wmin[d] = mine ? ac.winmin[(int64_t)d * ac.nwin + wi] : 0;
+      const int32_t wf = mine ? ac.win[wi] : -1;
       if (wb == w0) {  // the first chunk's flags were loaded with the node's operands
         KP_PP_MARK(0);
         if (nf != pass) return;
@@ -1024,29 +948,26 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
         Win<D, N32> wv[BATCH];
 #pragma unroll
         for (int t = 0; t < BATCH; ++t)
-          load_win<D, N32, COH>(wv[t], wl[t], lane, e0, e1, pass, ac.P, ac.bid, ac.ent_q,
+          load_win<D, N32>(wv[t], wl[t], lane, e0, e1, pass, ac.P, ac.bid, ac.ent_q,
                                 ac.ent_unit, ac.ent_size, ac.ent_lead, ac.ent_slot, ac.s0);
         KP_PP_MARK(2);
 #pragma unroll
         for (int t = 0; t < BATCH; ++t) {
           if (wl[t] < 0) break;
-          decide_window<D, N32, COH>(wv[t], rem, add, lane, node, o);
+          decide_window<D, N32>(wv[t], rem, add, lane, node, o);
         }
         KP_PP_MARK(3);
       }
     }
   }
   // fold the single-node units committed by this wave into `used`
-  bool any = false;
 #pragma unroll
   for (int d = 0; d < D; ++d) {
     const int64_t tot = (int64_t)readlane_nt((NT)(scan_excl<N32>(add[d]) + add[d]), 63);
     if (lane == 63 && tot != 0)
       atomicAdd(reinterpret_cast<unsigned long long *>(&o.used[(int64_t)d * N + node]),
                 (unsigned long long)tot);
-    any |= tot != 0;
   }
-  if (lane == 63 && any && o.chg) o.chg[node] = o.serial;
 }
 
 // One wave per node: the nodes with bidders this round (use_list: their
@@ -1065,521 +986,28 @@ __global__ __launch_bounds__(64 * KP_ACC_WPB) void k_accept(AccArgs ac, int32_t 
     const int4 r = ac.nrec[wv];
     const int32_t cnt = *ac.nl_count;
     if (wv >= cnt || !pf) return;
-    accept_node<D, N32, false, B>(ac, pass, r.x, r.y, r.z);
+    accept_node<D, N32, B>(ac, pass, r.x, r.y, r.z);
     for (int i = wv + nw; i < cnt; i += nw) {
       const int4 ri = ac.nrec[i];
-      accept_node<D, N32, false, B>(ac, pass, ri.x, ri.y, ri.z);
+      accept_node<D, N32, B>(ac, pass, ri.x, ri.y, ri.z);
     }
 #else
     const int32_t nd = ac.node_list[wv];
     const int32_t cnt = *ac.nl_count;
     if (wv >= cnt || !pf) return;
-    accept_node<D, N32, false, B>(ac, pass, nd, ac.seg_start[nd], ac.seg_end[nd]);
+    accept_node<D, N32, B>(ac, pass, nd, ac.seg_start[nd], ac.seg_end[nd]);
     for (int i = wv + nw; i < cnt; i += nw) {
       const int32_t ni = ac.node_list[i];
-      accept_node<D, N32, false, B>(ac, pass, ni, ac.seg_start[ni], ac.seg_end[ni]);
+      accept_node<D, N32, B>(ac, pass, ni, ac.seg_start[ni], ac.seg_end[ni]);
     }
 #endif
   } else {
     if (!pf) return;
     for (int node = wv; node < ac.sp.N; node += nw)
-      accept_node<D, N32, false, B>(ac, pass, node, ac.seg_start[node], ac.seg_end[node]);
+      accept_node<D, N32, B>(ac, pass, node, ac.seg_start[node], ac.seg_end[node]);
   }
 }
 
-// ---- persistent pass loop --------------------------------------------------------
-// All passes of a round in ONE launch of P resident workgroups (1,024 threads,
-// one per CU; P <= 64 << 256 CUs): plan -> grid barrier -> accept -> grid
-// barrier, until a pass without proposals or max_passes. The per-pass work is
-// exactly k_plan's and k_accept's (the same device functions with COH: the
-// pass state crosses workgroups write-through / past L1, usage by atomics),
-// so results are bit-identical to the launch-per-pass form; what goes is two
-// dependent kernel boundaries per pass (~16 us per pass pair at config #3,
-// DESIGN.md §5) in exchange for two barriers of ~1-1.5 us (tools/pass_barrier.hip).
-// Every spin is bounded: on a timeout the word err is set, the workgroups
-// leave, and the host fails the solve with KP_EHIP.
-struct LoopArgs {
-  int32_t *bar;   // arrival counter, zeroed at the round start (k_csr_keys / the merge)
-  int32_t *err;   // timeout flag, zeroed at the solve start
-  int32_t max_passes;
-};
-
-__device__ __forceinline__ bool grid_barrier(int32_t *bar, int32_t target, int32_t *err) {
-  // every storing wave drains its write-through stores before the workgroup
-  // signals for it (MI355X_MICROARCH.md § visibility: Valid forms, row 1)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  __shared__ int32_t s_ok;
-  if (threadIdx.x == 0) {
-    int32_t ok = 1;
-    __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
-          __builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {  // 0.5 s at 100 MHz
-        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
-    }
-    s_ok = ok;
-  }
-  __syncthreads();
-  return s_ok != 0;
-}
-
-#ifdef KP_LOOP_PROFILE
-// timing build: per (round, pass) the real-time stamps (100 MHz) of the loop's
-// phases: [0] pass start (min over workgroups), [1] last wave done planning
-// (before its stores drained), [2] plan stores drained (max over workgroups),
-// [3] barrier exit (min), [4] last wave done accepting, [5] accept drained,
-// [6] barrier exit; printed by kp_loop_profile_dump (kp_destroy)
-constexpr int kLP = 7;
-__device__ unsigned long long g_loop_prof[128][64][kLP];
-#define KP_LP(i, op)                                                                       \
-  do {                                                                                   \
-    if (threadIdx.x == 0 && pass < 64)                                                   \
-      op(&g_loop_prof[lp_round & 127][pass][i], (unsigned long long)__builtin_amdgcn_s_memrealtime()); \
-  } while (0)
-#define KP_LPW(i)                                                                          \
-  do {                                                                                   \
-    if ((threadIdx.x & 63) == 0 && pass < 64)                                            \
-      atomicMax(&g_loop_prof[lp_round & 127][pass][i], (unsigned long long)__builtin_amdgcn_s_memrealtime()); \
-  } while (0)
-#else
-#define KP_LP(i, op) \
-  do {               \
-  } while (0)
-#define KP_LPW(i) \
-  do {            \
-  } while (0)
-#endif
-
-template <int D, int G, bool W32, bool N32, int WPB>
-__global__ __launch_bounds__(64 * WPB) void k_pass_loop(PlanArgs pa, AccArgs ac, LoopArgs la) {
-  constexpr int SPW = 64 / G;  // slots per wave
-  const int wave_global = blockIdx.x * WPB + (threadIdx.x >> 6);
-  const int W = gridDim.x * WPB;
-  const int32_t P = (int32_t)gridDim.x;
-  const int32_t A = pa.A_dev ? min(pa.A, *pa.A_dev) : pa.A;
-  if (A <= 0) return;  // grid-uniform: nobody reaches a barrier
-  const int32_t cnt = *ac.nl_count;  // bid nodes of the round (k_csr_scan)
-#ifdef KP_LOOP_PROFILE
-  const int lp_round = (int)pa.st->rounds;
-#endif
-  int32_t phase = 0;
-  for (int32_t pass = 0; pass < la.max_passes; ++pass) {
-    KP_LP(0, atomicMin);
-    if (pass == 0) {
-      // per 64-entry window the smallest request per dim (k_plan pass 0's
-      // counting-mode prologue), published for the accepts
-      const int32_t ptot = *pa.ptot;
-      for (int64_t w = wave_global; w < pa.nwin; w += W) {
-        const int64_t e = w * 64 + (threadIdx.x & 63);
-        const bool ok = e < ptot;
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-          uint64_t x = ok ? (uint64_t)pa.ent_q[(int64_t)d * pa.P + e] : ~0ull;
-#pragma unroll
-          for (int m = 32; m >= 1; m >>= 1) {
-            const uint64_t o = shfl_xor_u64(x, m);
-            x = o < x ? o : x;
-          }
-          if ((threadIdx.x & 63) == 0) stc<true>(&pa.winmin[(int64_t)d * pa.nwin + w], (int64_t)x);
-        }
-      }
-    }
-    for (int g = wave_global; g * SPW < A; g += W) plan_wave<D, G, W32, true>(pa, pass, g);
-    KP_LPW(1);
-#ifdef KP_LOOP_PROFILE
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-#endif
-    KP_LP(2, atomicMax);
-    if (!grid_barrier(la.bar, P * ++phase, la.err)) return;
-    KP_LP(3, atomicMin);
-    // the same word on every workgroup after the barrier: all leave together
-    if (ldc<true>(&pa.pass_flag[pass]) == 0) break;
-    for (int i = wave_global; i < cnt; i += W) {
-      const int4 r = ac.nrec[i];
-      accept_node<D, N32, true>(ac, pass, r.x, r.y, r.z);
-    }
-    KP_LPW(4);
-#ifdef KP_LOOP_PROFILE
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-#endif
-    KP_LP(5, atomicMax);
-    if (!grid_barrier(la.bar, P * ++phase, la.err)) return;
-    KP_LP(6, atomicMin);
-  }
-}
-
-// ---- persistent pass loop, register-resident round state (k_pass_loop2) --------
-// The per-pass work of k_plan / k_accept is a chain of dependent loads
-// (slot -> unit / candidate -> node record + usage -> ...), ~6-7 us per phase
-// whether it runs as its own launch or inside a persistent one (k_pass_loop,
-// tools/gpu_loop_trace.sh). Almost all of it is static within a round: the
-// slot's unit, request and candidates, each candidate's node record and the
-// exact division of q·S. k_pass_loop2 gives every wave ONE slot group and at
-// most one bid node of the round for the whole launch, loads their static
-// operands once (prologue), and per pass reads only what changes: the
-// candidates' usage and the slot's placed flag (plan, one load level), the
-// node's pass flag, usage and window flags (accept, one level before its bid
-// windows). Same arithmetic as plan_wave's W32 form (every cap and request
-// < 2^32, D <= 4): bit-identical results.
-template <int D, int G>
-struct PlanReg {
-  int32_t a, u, sz, af, node, e_inv, nn, nbase, tp, abonus;
-  bool in, live;  // in: slot < A; live: the slot is open (cleared on fail / placed)
-  uint32_t q32[D], ncap[D], Q_[D], rho[D], thr[D], nR[D], nK[D];
-  int32_t wq[D];
-  uint32_t smask;
-};
-
-template <int D, int G>
-__device__ __forceinline__ void plan_reg_load(const PlanArgs &pa, int wave_global, int32_t A,
-                                              PlanReg<D, G> &r) {
-  constexpr int SPW = 64 / G;
-  const ScoreParams &sp = pa.sp;
-  const int lane = threadIdx.x & 63, gl = lane & (G - 1), gbase = lane & ~(G - 1);
-  const int K = sp.n_cand;
-  r.a = wave_global * SPW + lane / G;
-  const int aa = min(r.a, A - 1);
-  r.in = r.a < A;
-  const uint8_t op = pa.open[aa];
-  const int32_t u0 = pa.act[aa];
-  r.node = gl < K ? pa.cand[(int64_t)aa * K + gl] : -1;
-  r.e_inv = gl < K ? pa.inv[(int64_t)aa * K + gl] : 0;
-  r.live = r.in && op;
-  r.u = r.live ? u0 : 0;
-  r.sz = r.live ? pa.size[r.u] : 0;
-  r.af = r.live ? pa.aff[r.u] : -1;
-#pragma unroll
-  for (int d = 0; d < D; ++d) r.q32[d] = r.live ? (uint32_t)pa.q[(int64_t)d * pa.U + r.u] : 0u;
-  r.nn = r.live && r.node >= 0 ? r.node : 0;
-  const uint4 *rec = reinterpret_cast<const uint4 *>(pa.nst) + (int64_t)r.nn * 4;
-  const uint4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
-  const uint32_t c4[4] = {r0.x, r0.y, r0.z, r0.w}, R4[4] = {r1.x, r1.y, r1.z, r1.w},
-                 K4[4] = {r2.x, r2.y, r2.z, r2.w};
-  r.nbase = (int32_t)r3.x;
-  r.tp = (int32_t)r3.y;
-#pragma unroll
-  for (int d = 0; d < D; ++d) {
-    r.ncap[d] = c4[d];
-    r.nR[d] = R4[d];
-    r.nK[d] = K4[d];
-    divmod32(r.q32[d], r.ncap[d], r.nR[d], r.nK[d], (uint32_t)sp.S, r.Q_[d], r.rho[d]);
-    r.thr[d] = r.ncap[d] ? r.ncap[d] - r.rho[d] : 0xFFFFFFFFu;
-    r.wq[d] = sp.w[d] * (int32_t)r.Q_[d];
-  }
-  r.abonus = (r.af >= 0 && r.tp == r.af) ? sp.w_affinity : 0;
-  uint32_t sm = 0;
-#pragma unroll
-  for (int j = 0; j < G; ++j) sm |= (__shfl(r.tp, gbase + j, kWave) == r.tp ? 1u : 0u) << j;
-  r.smask = sm;
-}
-
-// one pass of plan_wave<D, G, true, true> on the register-resident slot group
-template <int D, int G>
-__device__ __forceinline__ void plan_reg_pass(const PlanArgs &pa, PlanReg<D, G> &r, int32_t pass) {
-  constexpr uint64_t GMASK = G == 64 ? ~0ull : ((1ull << G) - 1);
-  constexpr int LB = G == 16 ? 4 : G == 32 ? 5 : 6;
-  const ScoreParams &sp = pa.sp;
-  const int lane = threadIdx.x & 63, gl = lane & (G - 1), gbase = lane & ~(G - 1);
-  const int K = sp.n_cand, N = sp.N;
-  // the only per-pass loads: placed by an accept, and the candidates' usage
-  const int32_t done = pass > 0 && r.live ? ldc<true>(&pa.sdone[r.a]) : 0;
-  uint32_t uu[D];
-#pragma unroll
-  for (int d = 0; d < D; ++d) uu[d] = r.live ? (uint32_t)ldc<true>(&pa.used[(int64_t)d * N + r.nn]) : 0u;
-  if (pass == 0 && r.in && gl == 0) stc<true>(&pa.sdone[r.a], 0);
-  if (done) r.live = false;
-  const bool slot_ok = r.live;
-  if (__ballot(slot_ok) == 0) return;
-  const bool valid = slot_ok && r.node >= 0;
-  const int32_t sz = slot_ok ? r.sz : 0;
-  uint32_t rem[D], t_[D], r_[D];
-  int32_t acc_t = 0;
-#pragma unroll
-  for (int d = 0; d < D; ++d) {
-    rem[d] = r.ncap[d] - uu[d];
-    divmod32(uu[d] + r.q32[d], r.ncap[d], r.nR[d], r.nK[d], (uint32_t)sp.S, t_[d], r_[d]);
-    acc_t += sp.w[d] * (int32_t)t_[d];
-  }
-  const int g = sp.gpu_dim;
-  auto cur_score = [&]() -> int32_t {
-    bool fits = valid;
-    int32_t acc = acc_t, bonus = r.abonus;
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      fits &= r.q32[d] <= rem[d];
-      if (!sp.most_allocated && r_[d] != 0) acc += sp.w[d];
-      if (d == g && r.q32[d] > 0 && rem[d] == r.q32[d]) bonus += sp.w_gpu_fit;
-    }
-    return fits ? (sp.most_allocated ? acc : r.nbase - acc) + bonus : -1;
-  };
-  int32_t sc = cur_score();
-  const int32_t s0 = slot_ok ? sc : -1;
-  int32_t szmax = sz;
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) szmax = max(szmax, __shfl_xor(szmax, m, kWave));
-  int32_t planned = 0, pen = 0;
-  bool fail = !slot_ok;
-  for (int m = 0; m < szmax; ++m) {
-    const bool live = !fail && m < sz;  // group-uniform
-    const uint32_t key = (live && sc >= 0)
-                             ? ((uint32_t)(sc - pen + pa.key_off) << LB) | (uint32_t)(G - 1 - gl)
-                             : 0u;
-    const uint32_t best = group_max_u32<G>(key);
-    if (live && best == 0) fail = true;
-    if (live && !fail) {
-      const int w = G - 1 - (int)(best & (G - 1));
-      if (gl == w) {
-        ++planned;
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-          rem[d] -= r.q32[d];
-          const bool wrap = r_[d] >= r.thr[d];
-          t_[d] += r.Q_[d] + (wrap ? 1u : 0u);
-          r_[d] = wrap ? r_[d] - r.thr[d] : r_[d] + r.rho[d];
-          acc_t += r.wq[d] + (wrap ? sp.w[d] : 0);
-        }
-        sc = cur_score();
-      }
-      pen += (valid && ((r.smask >> w) & 1u)) ? sp.w_spread : 0;
-    }
-  }
-  const bool prop = slot_ok && !fail && gl < K && planned > 0;
-  const uint64_t pm = (__ballot(prop) >> gbase) & GMASK;
-  const int np = __popcll(pm);
-  const int32_t inc = group_incl_scan_i32<G>(planned);
-  if (!slot_ok) return;
-  if (fail) {
-    r.live = false;  // closed for the round (the slot's own register)
-    if (gl == 0 && pass == 0) pa.status[r.u] = kNoFit;
-    return;
-  }
-  if (prop) {
-    stc<true>(&pa.bid[r.e_inv], ((uint32_t)pass << 16) | ((uint32_t)np << 8) | (uint32_t)planned);
-    stc<true>(&pa.s0_out[r.e_inv], s0);
-    stc<true>(&pa.win[r.e_inv >> 6], pass);
-    stc<true>(&pa.node_flag[r.node], pass);
-    if (np > 1) {
-      const int idx = __popcll(pm & ((1ull << gl) - 1));
-      stc4<true>(&pa.gpart[(int64_t)r.a * K + idx], make_int4(r.node, planned, inc - planned, s0));
-    }
-  }
-  if (gl == 0) {
-    stc<true>(&pa.pass_flag[pass], 1);
-    if (np > 1) stc<true>(&pa.arrive[r.a], 0);
-  }
-}
-
-// accept of the wave's own bid node, its static operands in registers: the
-// row [e0, e1), capacity, and (from the first accept on) the window minima
-template <int D, bool N32>
-struct AccReg {
-  using NT = typename Win<D, N32>::NT;
-  int32_t node, e0, e1, w0, w1;
-  int64_t cap[D];
-  int64_t wmin[D];  // lane l: window w0 + l (l <= w1 - w0 < 64)
-  bool have;        // this wave owns a node of the round
-  bool wmin_ok;
-};
-
-template <int D, bool N32>
-__device__ __forceinline__ void accept_reg_pass(const AccArgs &ac, AccReg<D, N32> &n, int32_t pass) {
-  using NT = typename Win<D, N32>::NT;
-  const int lane = threadIdx.x & 63;
-  const int N = ac.sp.N;
-  const AcceptOut &o = ac.o;
-  if (n.w1 - n.w0 >= 64) {  // a row over more than 64 windows: the generic form
-    accept_node<D, N32, true>(ac, pass, n.node, n.e0, n.e1);
-    return;
-  }
-  const bool mine = lane <= n.w1 - n.w0;
-  // one level: pass flag, usage, window flags (+ window minima the first time)
-  const int32_t nf = ldc<true>(&ac.node_flag[n.node]);
-  int64_t uu[D];
-#pragma unroll
-  for (int d = 0; d < D; ++d) uu[d] = ldc<true>(&o.used[(int64_t)d * N + n.node]);
-  const int32_t wf = mine ? ldc<true>(&ac.win[n.w0 + lane]) : -1;
-  if (!n.wmin_ok) {
-#pragma unroll
-    for (int d = 0; d < D; ++d)
-      n.wmin[d] = mine ? ldc<true>(&ac.winmin[(int64_t)d * ac.nwin + n.w0 + lane]) : 0;
-    n.wmin_ok = true;
-  }
-  if (nf != pass) return;
-  NT rem[D], add[D];
-#pragma unroll
-  for (int d = 0; d < D; ++d) {
-    rem[d] = (NT)(n.cap[d] - uu[d]);
-    add[d] = 0;
-  }
-  constexpr int BATCH = KP_ACC_BATCH;
-  uint64_t flagged = __ballot(wf == pass);
-  while (true) {
-    bool can = true;
-#pragma unroll
-    for (int d = 0; d < D; ++d) can &= n.wmin[d] <= (int64_t)rem[d];
-    flagged &= __ballot(can);
-    if (!flagged) break;
-    int wl[BATCH];
-#pragma unroll
-    for (int t = 0; t < BATCH; ++t) {
-      wl[t] = flagged ? n.w0 + __ffsll((unsigned long long)flagged) - 1 : -1;
-      flagged &= flagged ? flagged - 1 : 0;
-    }
-    Win<D, N32> wv[BATCH];
-#pragma unroll
-    for (int t = 0; t < BATCH; ++t)
-      load_win<D, N32, true>(wv[t], wl[t], lane, n.e0, n.e1, pass, ac.P, ac.bid, ac.ent_q,
-                             ac.ent_unit, ac.ent_size, ac.ent_lead, ac.ent_slot, ac.s0);
-#pragma unroll
-    for (int t = 0; t < BATCH; ++t) {
-      if (wl[t] < 0) break;
-      decide_window<D, N32, true>(wv[t], rem, add, lane, n.node, o);
-    }
-  }
-  bool any = false;
-#pragma unroll
-  for (int d = 0; d < D; ++d) {
-    const int64_t tot = (int64_t)readlane_nt((NT)(scan_excl<N32>(add[d]) + add[d]), 63);
-    if (lane == 63 && tot != 0)
-      atomicAdd(reinterpret_cast<unsigned long long *>(&o.used[(int64_t)d * N + n.node]),
-                (unsigned long long)tot);
-    any |= tot != 0;
-  }
-  if (lane == 63 && any && o.chg) o.chg[n.node] = o.serial;
-}
-
-template <int D, int G, bool N32, int WPB>
-__global__ __launch_bounds__(64 * WPB) void k_pass_loop2(PlanArgs pa, AccArgs ac, LoopArgs la) {
-  const int wave_global = blockIdx.x * WPB + (threadIdx.x >> 6);
-  const int W = gridDim.x * WPB;
-  const int32_t P = (int32_t)gridDim.x;
-  const int32_t A = pa.A_dev ? min(pa.A, *pa.A_dev) : pa.A;
-  if (A <= 0) return;  // grid-uniform: nobody reaches a barrier
-  const int32_t cnt = *ac.nl_count;  // bid nodes of the round (k_csr_scan)
-  // prologue: static operands of this wave's slot group and bid node
-  PlanReg<D, G> pr;
-  plan_reg_load<D, G>(pa, wave_global, A, pr);
-  AccReg<D, N32> nr;
-  nr.have = wave_global < cnt;
-  nr.wmin_ok = false;
-  {
-    const int4 rc = ac.nrec[nr.have ? wave_global : 0];
-    nr.node = rc.x;
-    nr.e0 = rc.y;
-    nr.e1 = rc.z;
-    nr.w0 = rc.y >> 6;
-    nr.w1 = (rc.z - 1) >> 6;
-#pragma unroll
-    for (int d = 0; d < D; ++d) nr.cap[d] = nr.have ? ac.cap[(int64_t)d * ac.sp.N + rc.x] : 0;
-#pragma unroll
-    for (int d = 0; d < D; ++d) nr.wmin[d] = 0;
-  }
-  // per 64-entry window the smallest request per dim, published for the accepts
-  {
-    const int32_t ptot = *pa.ptot;
-    for (int64_t w = wave_global; w < pa.nwin; w += W) {
-      const int64_t e = w * 64 + (threadIdx.x & 63);
-      const bool ok = e < ptot;
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        uint64_t x = ok ? (uint64_t)pa.ent_q[(int64_t)d * pa.P + e] : ~0ull;
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) {
-          const uint64_t o = shfl_xor_u64(x, m);
-          x = o < x ? o : x;
-        }
-        if ((threadIdx.x & 63) == 0) stc<true>(&pa.winmin[(int64_t)d * pa.nwin + w], (int64_t)x);
-      }
-    }
-  }
-#ifdef KP_LOOP_PROFILE
-  const int lp_round = (int)pa.st->rounds;
-#endif
-  int32_t phase = 0;
-  for (int32_t pass = 0; pass < la.max_passes; ++pass) {
-    KP_LP(0, atomicMin);
-    plan_reg_pass<D, G>(pa, pr, pass);
-    KP_LPW(1);
-#ifdef KP_LOOP_PROFILE
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-#endif
-    KP_LP(2, atomicMax);
-    if (!grid_barrier(la.bar, P * ++phase, la.err)) return;
-    KP_LP(3, atomicMin);
-    if (ldc<true>(&pa.pass_flag[pass]) == 0) break;
-    if (nr.have) accept_reg_pass<D, N32>(ac, nr, pass);
-    for (int i = wave_global + W; i < cnt; i += W) {  // more bid nodes than waves
-      const int4 rc = ac.nrec[i];
-      accept_node<D, N32, true>(ac, pass, rc.x, rc.y, rc.z);
-    }
-    KP_LPW(4);
-#ifdef KP_LOOP_PROFILE
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-#endif
-    KP_LP(5, atomicMax);
-    if (!grid_barrier(la.bar, P * ++phase, la.err)) return;
-    KP_LP(6, atomicMin);
-  }
-}
-
-// ---- one-workgroup pass loop (k_pass_wg) -----------------------------------------
-// Every pass of a SMALL round in one 1,024-thread workgroup on one CU: plan
-// (16 waves over the slot groups) -> __syncthreads -> accept (16 waves over
-// the round's bid nodes) -> __syncthreads, until a pass without proposals or
-// max_passes. The per-pass work is k_plan's and k_accept's own device
-// functions in their launch-per-pass form (plain loads and stores, open[]):
-// within one workgroup __syncthreads orders global memory as a kernel
-// boundary does, with no grid barrier, no agent-scope hand-off and no launch
-// per phase. Only for rounds whose slots fit a few sweeps of the workgroup
-// (KP_PASS_WG_T); larger rounds need the whole GPU per pass.
-template <int D, int G, bool W32, bool N32>
-__global__ __launch_bounds__(1024) void k_pass_wg(PlanArgs pa, AccArgs ac, int32_t max_passes) {
-  constexpr int SPW = 64 / G;  // slots per wave
-  const int wave = threadIdx.x >> 6;
-  const int32_t A = pa.A_dev ? min(pa.A, *pa.A_dev) : pa.A;
-  if (A <= 0) return;  // workgroup-uniform
-  const int32_t cnt = *ac.nl_count;  // bid nodes of the round (k_csr_scan)
-  {  // k_plan pass 0's counting-mode prologue: per 64-entry window the
-     // smallest request per dim (accept's pruning bound)
-    const int32_t ptot = *pa.ptot;
-    for (int64_t w = wave; w < pa.nwin; w += 16) {
-      const int64_t e = w * 64 + (threadIdx.x & 63);
-      const bool ok = e < ptot;
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        uint64_t x = ok ? (uint64_t)pa.ent_q[(int64_t)d * pa.P + e] : ~0ull;
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) {
-          const uint64_t o = shfl_xor_u64(x, m);
-          x = o < x ? o : x;
-        }
-        if ((threadIdx.x & 63) == 0) pa.winmin[(int64_t)d * pa.nwin + w] = (int64_t)x;
-      }
-    }
-  }
-  for (int32_t pass = 0; pass < max_passes; ++pass) {
-    for (int g = wave; g * SPW < A; g += 16) plan_wave<D, G, W32>(pa, pass, g);
-    __syncthreads();  // bids, window / node / pass flags (and the winmin prologue)
-    if (pa.pass_flag[pass] == 0) break;  // the same word for every wave
-    for (int i = wave; i < cnt; i += 16) {
-      const int4 r = ac.nrec[i];
-      accept_node<D, N32>(ac, pass, r.x, r.y, r.z);
-    }
-    __syncthreads();  // usage, placements, closed slots
-  }
-}
-
-// the W32 member loop's key: largest score + 64 * w_spread + 1 < 2^(32 - lb)
 static bool plan_key_ok(const ScoreParams &sp, int lb) {
   int64_t bound = (int64_t)sp.w_gpu_fit + sp.w_affinity + 64 * (int64_t)sp.w_spread + 1;
   for (int d = 0; d < sp.D; ++d) bound += (int64_t)sp.w[d] * sp.S;
@@ -1629,7 +1057,6 @@ static PlanArgs plan_args(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t p
   pa.seg_end = c->d.seg_end;
   pa.nrec = c->d.nrec;
   pa.nst = c->d.nst;
-  pa.sdone = c->d.sdone;
   pa.pp = c->d.fz_prof ? c->d.fz_prof + 16 : nullptr;
   pa.st = c->d.stats;
   return pa;
@@ -1670,9 +1097,6 @@ static AccArgs acc_args(kp_ctx *c, const ScoreParams &sp, int64_t P) {
   o.status = c->d.status;
   o.job_node = c->d.job_node;
   o.job_score = c->d.job_score;
-  o.sdone = c->d.sdone;
-  o.chg = c->incr_active ? c->d.chg : nullptr;
-  o.serial = c->cur_serial;
   ac.hflag = c->hpass_on ? c->hpass : nullptr;
   ac.htag = (int32_t)(((uint32_t)c->cur_serial & 0x3FFFFFFFu) << 1);
   ac.pp = c->d.fz_prof ? c->d.fz_prof + 16 : nullptr;
@@ -1734,81 +1158,7 @@ struct AcceptL {
   }
 };
 
-// k_pass_loop workgroups: few waves each, so that the pass's divergent
-// gathers (candidate usage, node records) spread over many CUs' address units
-// (16-wave workgroups on 16 CUs: the plan phase took 10.5 us vs 7 us for the
-// same work as a k_plan launch over 64 CUs, tools/gpu_loop_trace.sh)
-#ifndef KP_LOOP_WPB
-#define KP_LOOP_WPB 4
-#endif
-template <int D>
-struct LoopL {
-  static int run(kp_ctx *c, const ScoreParams &sp, int32_t A, const int32_t *A_dev, int32_t P,
-                 int32_t max_passes) {
-    if constexpr (D > 4) {  // instantiated for the synthetic configs' D <= 4 only
-      return KP_ESTATE;
-    } else {
-    const PlanArgs pa = plan_args(c, sp, A, 0, A_dev);
-    const AccArgs ac = acc_args(c, sp, (int64_t)A * sp.n_cand);
-    LoopArgs la{c->d.pass_flag + kLoopBar, c->d.pass_flag + kLoopErr, max_passes};
-    const bool w32 = c->fits32 && plan_key_ok(sp, sp.n_cand <= 16 ? 4 : 5);
-    const bool n32 = c->fits32 && c->max_cap < ((int64_t)1 << 26);
-    const dim3 grid(P), blk(64 * KP_LOOP_WPB);
-    if (w32 && c->pass_loop_form == 2) {  // register-resident round state
-      if (sp.n_cand <= 16) {
-        if (n32) hipLaunchKernelGGL((k_pass_loop2<D, 16, true, KP_LOOP_WPB>), grid, blk, 0, c->stream, pa, ac, la);
-        else hipLaunchKernelGGL((k_pass_loop2<D, 16, false, KP_LOOP_WPB>), grid, blk, 0, c->stream, pa, ac, la);
-      } else {
-        if (n32) hipLaunchKernelGGL((k_pass_loop2<D, 32, true, KP_LOOP_WPB>), grid, blk, 0, c->stream, pa, ac, la);
-        else hipLaunchKernelGGL((k_pass_loop2<D, 32, false, KP_LOOP_WPB>), grid, blk, 0, c->stream, pa, ac, la);
-      }
-      KP_HIP(hipGetLastError());
-      return KP_OK;
-    }
-#define KP_LOOP(G_, W_, N_) \
-  hipLaunchKernelGGL((k_pass_loop<D, G_, W_, N_, KP_LOOP_WPB>), grid, blk, 0, c->stream, pa, ac, la)
-    if (sp.n_cand <= 16) {
-      if (w32) { if (n32) KP_LOOP(16, true, true); else KP_LOOP(16, true, false); }
-      else { if (n32) KP_LOOP(16, false, true); else KP_LOOP(16, false, false); }
-    } else {
-      if (w32) { if (n32) KP_LOOP(32, true, true); else KP_LOOP(32, true, false); }
-      else { if (n32) KP_LOOP(32, false, true); else KP_LOOP(32, false, false); }
-    }
-#undef KP_LOOP
-    KP_HIP(hipGetLastError());
-    return KP_OK;
-    }
-  }
-};
-
 }  // namespace
-
-template <int D>
-struct PassWgL {
-  static int run(kp_ctx *c, const ScoreParams &sp, int32_t A, const int32_t *A_dev,
-                 int32_t max_passes) {
-    if constexpr (D > 4) {  // instantiated for D <= 4 only
-      return KP_ESTATE;
-    } else {
-      const PlanArgs pa = plan_args(c, sp, A, 0, A_dev);
-      const AccArgs ac = acc_args(c, sp, (int64_t)A * sp.n_cand);
-      const bool w32 = c->fits32 && plan_key_ok(sp, sp.n_cand <= 16 ? 4 : 5);
-      const bool n32 = c->fits32 && c->max_cap < ((int64_t)1 << 26);
-#define KP_PWG(G_, W_, N_) \
-  hipLaunchKernelGGL((k_pass_wg<D, G_, W_, N_>), dim3(1), dim3(1024), 0, c->stream, pa, ac, max_passes)
-      if (sp.n_cand <= 16) {
-        if (w32) { if (n32) KP_PWG(16, true, true); else KP_PWG(16, true, false); }
-        else { if (n32) KP_PWG(16, false, true); else KP_PWG(16, false, false); }
-      } else {
-        if (w32) { if (n32) KP_PWG(32, true, true); else KP_PWG(32, true, false); }
-        else { if (n32) KP_PWG(32, false, true); else KP_PWG(32, false, false); }
-      }
-#undef KP_PWG
-      KP_HIP(hipGetLastError());
-      return KP_OK;
-    }
-  }
-};
 
 // CSR sort configuration: rounds with up to KP_SORT_SINGLE_BS x KP_SORT_SINGLE_IPT
 // entries sort in one workgroup (rocprim's default: 1,024); larger ones run the
@@ -1967,60 +1317,6 @@ int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev) {
 int launch_plan(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass, const int32_t *A_dev) {
   if (A <= 0) return KP_OK;
   return dispatch_D<PlanL>(c->D, c, sp, A, pass, A_dev);
-}
-
-// All passes of the round in one persistent launch when the round is small
-// enough for P <= pass_loop_pmax workgroups to hold one slot group per wave
-// and the bidder index is the counting form (node records from k_csr_scan).
-// Returns KP_OK with *done = false when the round takes the launch-per-pass form.
-void loop_profile_dump() {
-#ifdef KP_LOOP_PROFILE
-  static unsigned long long h[128][64][kLP];
-  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_loop_prof), sizeof h) != hipSuccess) return;
-  for (int r = 0; r < 128; ++r)
-    for (int p = 0; p < 64; ++p) {
-      const unsigned long long *x = h[r][p];
-      if (x[0] == 0 || x[0] == ~0ull) continue;
-      auto d = [&](int a, int b) {
-        return x[b] == 0 || x[b] == ~0ull ? 0.0 : (double)((long long)x[b] - (long long)x[a]) * 0.01;
-      };
-      std::fprintf(stderr, "kp_loop %d %d plan %.2f drain %.2f bar1 %.2f acc %.2f drain %.2f bar2 %.2f\n",
-                   r, p, d(0, 1), d(1, 2), d(2, 3), d(3, 4), d(4, 5), d(5, 6));
-    }
-#endif
-}
-
-void loop_profile_reset() {
-#ifdef KP_LOOP_PROFILE
-  static unsigned long long h[128][64][kLP];
-  for (int r = 0; r < 128; ++r)
-    for (int p = 0; p < 64; ++p)
-      for (int i = 0; i < kLP; ++i) h[r][p][i] = (i == 0 || i == 3 || i == 6) ? ~0ull : 0ull;
-  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_loop_prof), h, sizeof h);
-#endif
-}
-
-int launch_pass_loop(kp_ctx *c, const ScoreParams &sp, int32_t A, const int32_t *A_dev,
-                     int32_t max_passes, bool *done) {
-  *done = false;
-  if (!c->pass_loop_enabled || c->csr_mode != 1 || A <= 0 || c->N <= 0 || c->D > 4) return KP_OK;
-  const int32_t spw = sp.n_cand <= 16 ? 4 : 2;  // slots per wave (16- or 32-lane groups)
-  const int64_t P = ((int64_t)A + KP_LOOP_WPB * spw - 1) / (KP_LOOP_WPB * spw);
-  if (P > c->pass_loop_pmax) return KP_OK;
-  KP_TRY(dispatch_D<LoopL>(c->D, c, sp, A, A_dev, (int32_t)std::max<int64_t>(P, 1), max_passes));
-  *done = true;
-  return KP_OK;
-}
-
-int launch_pass_wg(kp_ctx *c, const ScoreParams &sp, int32_t A, const int32_t *A_dev,
-                   int32_t max_passes, bool *done) {
-  *done = false;
-  if (c->pass_wg_max <= 0 || A > c->pass_wg_max || c->csr_mode != 1 || A <= 0 || c->N <= 0 ||
-      c->D > 4)
-    return KP_OK;
-  KP_TRY(dispatch_D<PassWgL>(c->D, c, sp, A, A_dev, max_passes));
-  *done = true;
-  return KP_OK;
 }
 
 int launch_accept(kp_ctx *c, const ScoreParams &sp, int32_t pass, int32_t A) {

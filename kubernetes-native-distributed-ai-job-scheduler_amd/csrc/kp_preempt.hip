@@ -310,7 +310,10 @@ __global__ void k_preempt_init(int32_t J, int32_t *__restrict__ node, int32_t *_
 template <int D>
 struct PreemptL {
   static int run(kp_ctx *c, int32_t P) {
-    if (c->fits32 && c->preempt32 && c->pre_key_ok) {
+    // the tiled kernel sums free capacity and evictable requests in u32: after
+    // kp_apply_delta lowers usage below the running jobs' sum, that sum can
+    // reach ~2 x cap, so it needs every cap < 2^31
+    if (c->fits32 && c->preempt32 && c->pre_key_ok && c->max_cap < ((int64_t)1 << 31)) {
       hipLaunchKernelGGL((k_preempt_t<D>), dim3(blocks(P, kPtRows)), dim3(256), 0, c->stream, c->N,
                          c->U, P, c->R, c->d.plist, c->d.q, c->d.uprio, c->d.leader, c->d.cap,
                          c->d.used, c->d.roff, c->d.rreq, c->d.rsuf, c->d.rprio, c->d.pre_node,

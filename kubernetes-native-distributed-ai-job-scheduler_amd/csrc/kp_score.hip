@@ -1030,42 +1030,25 @@ __global__ __launch_bounds__(kCompactBS) void k_round_begin(
     const uint32_t *__restrict__ R32, const uint32_t *__restrict__ K32,
     const int64_t *__restrict__ base, const int32_t *__restrict__ topo,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ colnode, int32_t N, int32_t P,
-    int32_t full, ScoreParams sp, uint32_t *__restrict__ np, const int32_t *__restrict__ chg,
-    int32_t serial_prev, int32_t *__restrict__ clist, int32_t *__restrict__ ccount) {
+    int32_t full, ScoreParams sp, uint32_t *__restrict__ np) {
   if (blockIdx.x == 0) {
     compact_wg<true>(status, n, lo, out, count, host_count);
     return;
   }
   const int i = (blockIdx.x - 1) * kCompactBS + threadIdx.x;
   if (i < P) pack_node<D>(cap, used, R32, K32, base, topo, perm, colnode, N, P, full != 0, sp, np, i);
-  if (chg) {  // incremental candidate phase: the nodes the previous round changed
-    const int32_t nd = i < P ? colnode[i] : -1;
-    const bool hit = nd >= 0 && chg[nd] == serial_prev;
-    const uint64_t m = __ballot(hit);
-    if (m) {
-      int32_t b = 0;
-      if ((threadIdx.x & 63) == 0) b = atomicAdd(ccount, __popcll(m));
-      b = __shfl(b, 0, 64);
-      if (hit) clist[b + mbcnt64(m)] = nd;
-    }
-  }
 }
 
 template <int D>
 struct RoundBeginL {
   static int run(kp_ctx *c, int32_t lo, int32_t n, int32_t *host_count) {
     const int32_t P = !c->fits32 || c->N == 0 ? 0 : c->pack_fused ? c->fz_P : (c->N + 1023) & ~1023;
-    // incremental rounds after the first: compact the nodes the previous
-    // round's passes changed (the fused layout's columns cover every node)
-    const bool chg = c->incr_active && c->incr_round > 0 && c->pack_fused && P > 0;
-    const int par = c->incr_round & 1;
     hipLaunchKernelGGL((k_round_begin<D>), dim3(1 + blocks(P, kCompactBS)), dim3(kCompactBS), 0,
                        c->stream, c->d.status, lo, n, c->d.act_local, c->d.counters, host_count,
                        c->d.cap, c->d.used, c->d.R32, c->d.K32, c->d.base, c->d.topo,
                        c->pack_canonical ? c->d.perm : nullptr,
                        c->pack_fused ? c->d.colnode : nullptr, c->N, P, c->pack_full ? 1 : 0,
-                       c->pack_sp, c->d.np32, chg ? c->d.chg : nullptr, c->cur_serial - 1,
-                       c->d.clist + (size_t)par * c->cap_N, c->d.counters + kCCount + par);
+                       c->pack_sp, c->d.np32);
     KP_HIP(hipGetLastError());
     if (P > 0) c->pack_full = false;  // capacity planes in place for this layout
     return KP_OK;

@@ -556,11 +556,6 @@ void k_score_topk(
 // max of the heads, and only the owner of the max advances its list (one LDS
 // read). K x (one wave max + one LDS read) per row instead of K passes over
 // all ntiles*K keys. Dynamic LDS: 4 rows x ntiles*K keys.
-// List mode (lo.ukey, the incremental candidate phase, kp_incr.hip): K is the
-// list length KL >= the solve's n_cand (lo.kout); the row's top-KL keys and
-// nodes, their count and the bound (the KL-th key, 0 = every feasible node is
-// listed) go to the unit's list, the first kout nodes to cand at the row's
-// slot (lo.rslot: row -> slot, the rescan rows of a round).
 template <int LPL>
 __global__ __launch_bounds__(64 * KP_MERGE_WPB) void k_merge_tour(ScoreParams sp, const uint64_t *__restrict__ part,
                                                     int32_t ntiles,
@@ -568,8 +563,7 @@ __global__ __launch_bounds__(64 * KP_MERGE_WPB) void k_merge_tour(ScoreParams sp
                                                     const uint32_t *__restrict__ salt, int32_t rows,
                                                     const int32_t *__restrict__ rows_dev,
                                                     const int32_t *__restrict__ perm,
-                                                    int32_t *__restrict__ cand, RoundKeys rk,
-                                                    ListOut lo) {
+                                                    int32_t *__restrict__ cand, RoundKeys rk) {
   extern __shared__ uint64_t slist[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int rblocks = (rows + kMergeWPB - 1) / kMergeWPB;
@@ -600,8 +594,7 @@ __global__ __launch_bounds__(64 * KP_MERGE_WPB) void k_merge_tour(ScoreParams sp
   // lane it keeps the canonical position of candidate it; the positions are
   // mapped to nodes after the loop with ONE load per lane (a perm load + store
   // inside the loop serialises K memory latencies)
-  int32_t mypos = -1, got = 0;
-  uint64_t mykey = 0;
+  int32_t mypos = -1;
   for (int it = 0; it < K; ++it) {
     uint64_t b = v[0];
 #pragma unroll
@@ -617,39 +610,18 @@ __global__ __launch_bounds__(64 * KP_MERGE_WPB) void k_merge_tour(ScoreParams sp
         ++h[j];
         v[j] = h[j] < K ? L[t * K + h[j]] : 0ull;
       }
-    if (lane == it) {
-      mypos = key_node(m, sl, inv);
-      mykey = m;
-    }
-    got = it + 1;
+    if (lane == it) mypos = key_node(m, sl, inv);
   }
   // canonical position -> node (a position is always < N)
   const int32_t mine = (uint32_t)mypos < (uint32_t)sp.N ? perm[mypos] : -1;
-  const int kout = lo.ukey ? lo.kout : K;
-  const int32_t slot = lo.rslot ? lo.rslot[row] : row;
-  if (lane < kout) cand[(int64_t)slot * kout + lane] = mine;
-  if (lo.ukey) {
-    // the list: a bound below every unlisted node's key, or 0 when fewer than
-    // K keys exist (some tile ran out: every feasible node is listed)
-    const int64_t lb = (int64_t)unit * K;
-    if (lane < K) {
-      lo.ukey[lb + lane] = mykey;
-      lo.unode[lb + lane] = mine;
-    }
-    const uint64_t bound = got == K ? (uint64_t)readlane_i64((int64_t)mykey, K - 1) : 0ull;
-    if (lane == 0) {
-      lo.ucnt[unit] = got;
-      lo.ubound[unit] = bound;
-    }
-  }
-  if (rk.enabled) round_keys_slot(rk, slot, unit, kout, mine, lane);  // k_csr_keys' work for the slot
+  if (lane < K) cand[(int64_t)row * K + lane] = mine;
+  if (rk.enabled) round_keys_slot(rk, row, unit, K, mine, lane);  // k_csr_keys' work for the slot
 }
 
 template <int D>
 struct TopkL {
   static int run(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
-                 int32_t ksh, int32_t *cand, const int32_t *rows_dev, const ListOut &lo,
-                 bool init_wgs) {
+                 int32_t ksh, int32_t *cand, const int32_t *rows_dev, bool init_wgs) {
     const int P = c->fz_P, ntiles = P / kFzTile;
     const int64_t want = ((int64_t)rows * ntiles + c->fz_wg_target - 1) / c->fz_wg_target;
     const int rpb = (int)std::min<int64_t>(kFzMaxRows, std::max<int64_t>(kFzRC, want));
@@ -671,14 +643,13 @@ struct TopkL {
     if (c->fz_end_event) KP_HIP(hipEventRecord(c->fz_end_event, c->stream));
     const int M = ntiles * sp.n_cand;
     RoundKeys rk{};
-    // the slots' keys work uses the solve's K (lo.kout in list mode)
-    if (c->keys_in_merge) rk = round_keys_args(c, rows, lo.ukey ? lo.kout : sp.n_cand, c->d.counters);
+    if (c->keys_in_merge) rk = round_keys_args(c, rows, sp.n_cand, c->d.counters);
     const dim3 mg(blocks(rows, kMergeWPB) +
                   (rk.enabled && init_wgs ? blocks(rk.init_n, 64 * kMergeWPB) : 0));
     const size_t lds = (size_t)kMergeWPB * M * sizeof(uint64_t);  // <= 16 KB per row (M <= 2,048)
 #define KP_MG(LPL)                                                                       \
   hipLaunchKernelGGL((k_merge_tour<LPL>), mg, dim3(64 * kMergeWPB), lds, c->stream, sp, c->d.part, \
-                     ntiles, rows_unit, c->d.salt, rows, rows_dev, c->d.perm, cand, rk, lo)
+                     ntiles, rows_unit, c->d.salt, rows, rows_dev, c->d.perm, cand, rk)
     if (ntiles <= 64)
       KP_MG(1);
     else if (ntiles <= 128)
@@ -700,10 +671,9 @@ struct TopkL {
 }  // namespace
 
 int launch_score_topk(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
-                      int32_t ksh, int32_t *cand, const int32_t *rows_dev, const ListOut &lo,
-                      bool init_wgs) {
+                      int32_t ksh, int32_t *cand, const int32_t *rows_dev, bool init_wgs) {
   if (rows <= 0 || c->N == 0) return KP_OK;
-  return dispatch_D<TopkL>(c->D, c, sp, rows_unit, rows, ksh, cand, rows_dev, lo, init_wgs);
+  return dispatch_D<TopkL>(c->D, c, sp, rows_unit, rows, ksh, cand, rows_dev, init_wgs);
 }
 
 }  // namespace kp

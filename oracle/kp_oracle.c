@@ -398,6 +398,11 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
   const char *trace_env = getenv("KPO_TRACE"); /* per-round counts on stderr (analysis) */
   const int trace = trace_env ? (atoi(trace_env) > 1 ? 2 : 1) : 0;
   int32_t passes0 = st->passes;
+  int32_t *chg_pass = NULL; /* KPO_TRACE=2 analysis: last pass that changed each node's usage */
+  if (trace > 1) {
+    chg_pass = (int32_t *)malloc(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
+    for (int32_t n = 0; chg_pass && n < N; ++n) chg_pass[n] = -2;
+  }
   for (int pass = 0; pass < st->p.max_passes; ++pass) {
     /* proposals of every open unit, planned against the current usage */
     int32_t np = 0;
@@ -414,10 +419,21 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
     st->passes++;
     qsort(props, np, sizeof *props, cmp_prop);
     if (trace > 1) { /* KPO_TRACE=2: per-pass open units, proposals, bid nodes */
-      int32_t nopen = 0, nodes = 0;
+      int32_t nopen = 0, nodes = 0, dirty = 0, nchg = 0;
       for (int32_t u = 0; u < U; ++u) nopen += open[u];
       for (int32_t k = 0; k < np; ++k) nodes += k == 0 || props[k].node != props[k - 1].node;
-      fprintf(stderr, "kpo pass %d.%d open %d props %d nodes %d\n", st->rounds, pass, nopen, np, nodes);
+      if (chg_pass) { /* open units with a candidate whose usage the previous pass changed */
+        for (int32_t n = 0; n < N; ++n) nchg += chg_pass[n] == pass - 1;
+        for (int32_t u = 0; u < U; ++u) {
+          if (!open[u]) continue;
+          int d = pass == 0;
+          for (int k = 0; k < K && !d && cand[(size_t)u * K + k] >= 0; ++k)
+            d = chg_pass[cand[(size_t)u * K + k]] == pass - 1;
+          dirty += d;
+        }
+      }
+      fprintf(stderr, "kpo pass %d.%d open %d props %d nodes %d changed %d dirty %d\n", st->rounds, pass,
+              nopen, np, nodes, nchg, dirty);
     }
     /* per node, in unit rank order: first-fit against the remaining capacity */
     int64_t rem[KP_MAX_DIMS];
@@ -449,6 +465,7 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
       unit_req(st, u, q);
       for (int d = 0; d < D; ++d)
         st->used[(int64_t)d * N + props[k].node] += (int64_t)props[k].count * q[d];
+      if (chg_pass) chg_pass[props[k].node] = pass;
       for (int32_t m = 0; m < props[k].count; ++m) {
         st->job_node[st->leader[u] + props[k].member_off + m] = props[k].node;
         st->job_score[st->leader[u] + props[k].member_off + m] = props[k].score;
@@ -460,6 +477,7 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
   if (trace)
     fprintf(stderr, "kpo round %d active %d passes %d\n", st->rounds, active0, st->passes - passes0);
   st->rounds++;
+  free(chg_pass);
   free(open); free(props); free(ok); free(gang_bad);
   return kpo_state_active(st);
 }

@@ -269,52 +269,6 @@ def test_csr_build_paths_parity(oracle, monkeypatch, knobs):
     _assert_same(g2, o, f"csr {knobs} second solve")
 
 
-@pytest.mark.parametrize("form", ["1", "2"])
-@pytest.mark.parametrize("pmax,cfg", [("64", (3, 20_000, 2_000)), ("256", (3, 20_000, 2_000)),
-                                      ("8", (2, 6_000, 600)), ("64", (4, 8_000, 1_500))])
-def test_pass_loop_parity(oracle, monkeypatch, form, pmax, cfg):
-    """The persistent pass loop (KP_PASS_LOOP=1, a measured alternative that
-    is off by default): every pass of a qualifying round in one launch of
-    resident workgroups with grid barriers; form 1 reloads the pass state,
-    form 2 keeps each wave's slot group and bid node in registers. Same
-    placement, rounds and passes as the oracle."""
-    monkeypatch.setenv("KP_PASS_LOOP", "1")
-    monkeypatch.setenv("KP_PASS_LOOP_FORM", form)
-    monkeypatch.setenv("KP_PASS_LOOP_PMAX", pmax)
-    no, J, N = cfg
-    w = synth.config(no, J, N)
-    p = _abi.default_params(**synth.CONFIG_PARAMS[no])
-    with Placer(device=0) as pl:
-        g = pl.place(w, p)
-        looped = pl.timing()["loop_rounds"]
-        g2 = pl.place(w, p)
-    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
-    assert looped > 0, "no round took the pass loop"
-    _assert_same(g, o, f"pass loop form {form} pmax {pmax}")
-    _assert_same(g2, o, f"pass loop form {form} pmax {pmax}, second solve")
-
-
-@pytest.mark.parametrize("T", ["64", "512", "4096", "1000000"])
-@pytest.mark.parametrize("cfg", [(3, 20_000, 2_000), (2, 6_000, 600), (4, 8_000, 1_500)])
-def test_pass_wg_parity(oracle, monkeypatch, T, cfg):
-    """The one-workgroup pass loop (KP_PASS_WG_T = T): every pass of a round
-    with at most T slots in one 1,024-thread workgroup, __syncthreads between
-    plan and accept. T = 1,000,000 takes every round of these snapshots.
-    Same placement, rounds and passes as the oracle; a second solve too."""
-    monkeypatch.setenv("KP_PASS_WG_T", T)
-    no, J, N = cfg
-    w = synth.config(no, J, N)
-    p = _abi.default_params(**synth.CONFIG_PARAMS[no])
-    with Placer(device=0) as pl:
-        g = pl.place(w, p)
-        looped = pl.timing()["loop_rounds"]
-        g2 = pl.place(w, p)
-    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
-    assert looped > 0, "no round took the one-workgroup loop"
-    _assert_same(g, o, f"pass wg T {T} cfg {cfg}")
-    _assert_same(g2, o, f"pass wg T {T} cfg {cfg}, second solve")
-
-
 @pytest.mark.parametrize("M", ["0", "1", "2", "3", "15", "16"])
 @pytest.mark.parametrize("cfg", [(3, 20_000, 2_000, 16), (4, 8_000, 1_500, 16), (2, 6_000, 600, 3)])
 def test_pass_follow_parity(oracle, monkeypatch, M, cfg):
@@ -358,32 +312,6 @@ def test_accept_long_row_form_parity(oracle, monkeypatch, seed):
     o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
     _assert_same(g, o, f"accept long-row form seed {seed}")
     _assert_same(g2, o, f"accept long-row form seed {seed}, second solve")
-
-
-def test_pass_wg_random_parity(oracle, monkeypatch):
-    """The one-workgroup loop on random snapshots: gangs spread over several
-    nodes, both score modes, D <= 4, 32-candidate lists (32-lane groups)."""
-    monkeypatch.setenv("KP_PASS_WG_T", "1000000")
-    for seed, D, K, mode in ((3, 4, 16, 0), (4, 3, 32, 1), (5, 2, 8, 0), (6, 1, 16, 1)):
-        w = random_workload(600 + seed, J=3_000, N=400, D=D)
-        p = _abi.default_params(n_cand=K, score_mode=mode, gpu_dim=min(2, D - 1))
-        with Placer(device=0) as pl:
-            g = pl.place(w, p)
-        o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
-        _assert_same(g, o, f"pass wg random seed {seed}")
-
-
-def test_pass_loop_random_parity(oracle, monkeypatch):
-    """The pass loop on random snapshots with gangs, both score modes, D <= 4
-    (the loop's instantiations) and 32-candidate lists."""
-    monkeypatch.setenv("KP_PASS_LOOP", "1")
-    for seed, D, K, mode in ((3, 4, 16, 0), (4, 3, 32, 1), (5, 2, 8, 0), (6, 1, 16, 1)):
-        w = random_workload(500 + seed, J=3_000, N=400, D=D)
-        p = _abi.default_params(n_cand=K, score_mode=mode, gpu_dim=min(2, D - 1))
-        with Placer(device=0) as pl:
-            g = pl.place(w, p)
-        o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
-        _assert_same(g, o, f"pass loop random seed {seed}")
 
 
 def test_csr_scan_many_nodes(oracle):
