@@ -287,6 +287,14 @@ def main():
     ap.add_argument("--single-process", action="store_true",
                     help="drive --gpus N GPUs from this process (kp_create_multi)")
     ap.add_argument("--master-port", type=int, default=29533)
+    ap.add_argument("--exchange", choices=("rccl", "host"), default="rccl",
+                    help="candidate exchange of a multi-rank run: RCCL (one GPU per rank), or "
+                         "host-staged over the gloo group (rehearsal of the multi-rank code on a "
+                         "box with fewer GPUs than ranks: rank r uses GPU r mod count; not a "
+                         "perf number)")
+    ap.add_argument("--gpu-ids", default=None,
+                    help="--single-process: comma-separated GPU ids (a repeated id runs the "
+                         "in-process exchange; rehearsal only)")
     ap.add_argument("--place-steps", type=int, default=5, help="kp_place (host->host) repetitions")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-single-sample", type=float, default=1.0,
@@ -328,16 +336,35 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
     nid = None
-    if world > 1:
+    if world > 1 and args.exchange == "rccl":
         obj = [unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         nid = obj[0]
 
+    rehearsal = False
     if args.single_process:
-        ids = list(range(args.gpus))
+        ids = [int(x) for x in args.gpu_ids.split(",")] if args.gpu_ids else list(range(args.gpus))
+        if len(ids) != args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} but --gpu-ids names {len(ids)} GPUs")
+        rehearsal = len(set(ids)) < len(ids)
         make_placer = lambda: Placer(gpu_ids=ids)  # noqa: E731
         parallelism = f"job-row shards x{args.gpus} (one process, kp_create_multi)"
         n_gpus = args.gpus
+    elif world > 1 and args.exchange == "host":
+        import torch
+
+        def allgather(data: bytes) -> bytes:  # host-staged exchange over the gloo group
+            t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+            bufs = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(bufs, t)
+            return b"".join(b.numpy().tobytes() for b in bufs)
+
+        dev = local % max(1, torch.cuda.device_count())
+        rehearsal = True
+        make_placer = lambda: Placer(device=dev, world_size=world, rank=rank,  # noqa: E731
+                                     allgather=allgather)
+        parallelism = f"job-row shards x{world} (host-staged exchange)"
+        n_gpus = world
     else:
         make_placer = lambda: Placer(device=local, world_size=world, rank=rank,  # noqa: E731
                                      nccl_id=nid)
@@ -446,7 +473,8 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "int64",
-        "data": "synthetic (splitmix64 config #3 generator, SURVEY.md §8d)",
+        "data": "synthetic (splitmix64 config #3 generator, SURVEY.md §8d)" +
+                (" [REHEARSAL: several ranks share one GPU; not a perf number]" if rehearsal else ""),
         "config": {"workload": "config3: 100k jobs x 10k nodes x 4 dims, gangs {1,2,4,8}, "
                                "A/B 8-GPU nodes, bin-pack + spread + GPU-fit",
                    "jobs": args.jobs, "nodes": args.nodes, "dims": 4,

@@ -689,38 +689,45 @@ static int wait_stream(kp_ctx *c, hipEvent_t ev) {
 }
 
 // ---------------------------------------------------------------------------
+// One all-gather of `per` int32 per rank (device send [per] -> device recv
+// [world][per]) over the context's transport: RCCL over xGMI, or the
+// host-staged callback (kp_set_allgather, or the in-process exchange of
+// kp_create_multi with a repeated GPU id) through host memory.
+static int allgather_i32(kp_ctx *c, const int32_t *send, int32_t *recv, size_t per) {
+  if (c->nccl_comm) {
+    if (c->peer_failed && c->peer_failed->load(std::memory_order_acquire))
+      return fail(KP_ERCCL, "a peer shard failed before the exchange");
+    c->in_collective = true;
+    if (ncclAllGather(send, recv, per, ncclInt32, static_cast<ncclComm_t>(c->nccl_comm),
+                      c->stream) != ncclSuccess)
+      return fail(KP_ERCCL, "ncclAllGather of %zu ints", per);
+    return KP_OK;
+  }
+  try {
+    c->h_xg_send.resize(per);
+    c->h_xg_recv.resize(per * c->world);
+  } catch (const std::bad_alloc &) {
+    return fail(KP_ENOMEM, "exchange staging");
+  }
+  KP_HIP(hipMemcpyAsync(c->h_xg_send.data(), send, sizeof(int32_t) * per, hipMemcpyDeviceToHost,
+                        c->stream));
+  KP_HIP(hipStreamSynchronize(c->stream));
+  if (c->allgather(c->allgather_user, c->h_xg_send.data(), sizeof(int32_t) * per,
+                   c->h_xg_recv.data()) != 0)
+    return fail(KP_ERCCL, "host-staged all-gather failed");
+  KP_HIP(hipMemcpyAsync(recv, c->h_xg_recv.data(), sizeof(int32_t) * per * c->world,
+                        hipMemcpyHostToDevice, c->stream));
+  return KP_OK;
+}
+
 // This rank's candidates -> every rank's, as fixed-size blocks
 // [count, (unit, K candidates) x B] (B: the same slot bound on every rank), so
 // the all-gather needs no host-known count: one collective per round and, over
-// RCCL, no host synchronisation. The host-staged transport (kp_set_allgather,
-// or the in-process exchange of kp_create_multi) moves the same blocks
-// through host memory.
+// RCCL, no host synchronisation.
 static int exchange_round(kp_ctx *c, int32_t B, int32_t K) {
   const size_t per = 1 + (size_t)B * (K + 1);
   KP_TRY(launch_pack_exchange(c, B, K));
-  if (c->nccl_comm) {
-    if (c->peer_failed && c->peer_failed->load(std::memory_order_acquire))
-      return fail(KP_ERCCL, "kp_solve: a peer shard failed before the exchange");
-    c->in_collective = true;
-    if (ncclAllGather(c->d.xg_send, c->d.xg_recv, per, ncclInt32,
-                      static_cast<ncclComm_t>(c->nccl_comm), c->stream) != ncclSuccess)
-      return fail(KP_ERCCL, "ncclAllGather of %zu ints", per);
-  } else {
-    try {
-      c->h_xg_send.resize(per);
-      c->h_xg_recv.resize(per * c->world);
-    } catch (const std::bad_alloc &) {
-      return fail(KP_ENOMEM, "exchange staging");
-    }
-    KP_HIP(hipMemcpyAsync(c->h_xg_send.data(), c->d.xg_send, sizeof(int32_t) * per,
-                          hipMemcpyDeviceToHost, c->stream));
-    KP_HIP(hipStreamSynchronize(c->stream));
-    if (c->allgather(c->allgather_user, c->h_xg_send.data(), sizeof(int32_t) * per,
-                     c->h_xg_recv.data()) != 0)
-      return fail(KP_ERCCL, "host-staged all-gather failed");
-    KP_HIP(hipMemcpyAsync(c->d.xg_recv, c->h_xg_recv.data(), sizeof(int32_t) * per * c->world,
-                          hipMemcpyHostToDevice, c->stream));
-  }
+  KP_TRY(allgather_i32(c, c->d.xg_send, c->d.xg_recv, per));
   return launch_unpack_exchange(c, c->world, B, K);
 }
 
@@ -1277,7 +1284,7 @@ void kp_destroy(kp_ctx *c) {
                   d.ent_slot, d.ent_size, d.ent_lead, d.ent_q, d.perm,
                   d.csr_kin, d.csr_vin,
                   d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
-                  d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.roff,
+                  d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.pre_send, d.pre_recv, d.roff,
                   d.rreq, d.rsuf, d.rprio, d.pre_node, d.pre_vict, d.pre_cost,
                   d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.nrec, d.nst, d.stats, d.np32, d.colnode, d.wshift, d.part, d.fz_prof,
                   d.bm, d.rowinfo, d.cnt};
@@ -1488,9 +1495,9 @@ int kp_score(kp_ctx *c, const kp_params *p, int32_t job_lo, int32_t job_hi, int3
 int kp_load_running(kp_ctx *c, int32_t R, const int32_t *node, const int64_t *req,
                     const int32_t *prio) {
   if (!c) return KP_EINVAL;
-  if (c->multi)  // preemption runs on shard 0 only (kp_preempt)
+  if (c->multi)  // every shard scores its share of the preemptors (kp_preempt)
     return multi_run(c, [&](kp_ctx *sh, int) { return kp_load_running(sh, R, node, req, prio); },
-                     false);
+                     true);
   Entry en(c);
   if (!c->nodes_loaded) return fail(KP_ESTATE, "kp_load_running: no node table loaded");
   if (R < 0 || (R > 0 && (!node || !req || !prio)))
@@ -1588,12 +1595,38 @@ int kp_load_running(kp_ctx *c, int32_t R, const int32_t *node, const int64_t *re
 
 int kp_preempt(kp_ctx *c, kp_preemption *out) {
   if (!c || !out) return KP_EINVAL;
-  if (c->multi) return multi_run(c, [&](kp_ctx *sh, int) { return kp_preempt(sh, out); }, false);
+  if (c->multi) {
+    // every shard scores its rows and all-gathers them (identical outputs on
+    // every shard); shard 0 writes the caller's arrays
+    std::vector<kp_preemption> outs(c->world, kp_preemption{});
+    const int rc = multi_run(c, [&](kp_ctx *sh, int i) {
+      if (i == 0) return kp_preempt(sh, out);
+      return kp_preempt(sh, &outs[i]);  // counts only, no arrays
+    }, true);
+    return rc;
+  }
   Entry en(c);
   if (!c->solved) return fail(KP_ESTATE, "kp_preempt: no solve since the last load");
   KP_HIP(hipSetDevice(c->device));
-  int32_t P = 0;
-  KP_TRY(launch_preempt(c, &P));
+  int32_t P = 0, lo = 0, hi = 0;
+  KP_TRY(launch_preempt(c, &P, &lo, &hi));
+  if (c->world > 1 && P > 0) {
+    // rank r scored rows [lo, hi): one all-gather of B = ceil(P / world) rows
+    // per rank gives every rank every nomination
+    if (!c->nccl_comm && !c->allgather)
+      return fail(KP_ESTATE, "kp_preempt: multi-rank context without an exchange");
+    const int32_t B = (int32_t)(((int64_t)P + c->world - 1) / c->world);
+    const int64_t per = (int64_t)B * 4;
+    if (per > c->cap_pre_xg || !c->d.pre_send || !c->d.pre_recv) {
+      c->cap_pre_xg = 0;
+      KP_TRY(dalloc(&c->d.pre_send, (size_t)per));
+      KP_TRY(dalloc(&c->d.pre_recv, (size_t)per * c->world));
+      c->cap_pre_xg = per;
+    }
+    KP_TRY(launch_preempt_pack(c, lo, hi, c->d.pre_send));
+    KP_TRY(allgather_i32(c, c->d.pre_send, c->d.pre_recv, (size_t)per));
+    KP_TRY(launch_preempt_unpack(c, P, B, c->d.pre_recv));
+  }
   const int32_t J = c->J;
   if (J > 0) {
     if (out->node_of_job)
@@ -1610,7 +1643,15 @@ int kp_preempt(kp_ctx *c, kp_preemption *out) {
   if (J > 0)
     KP_HIP(hipMemcpyAsync(nom.data(), c->d.pre_node, sizeof(int32_t) * J, hipMemcpyDeviceToHost,
                           c->stream));
-  KP_HIP(hipStreamSynchronize(c->stream));
+  if (c->world > 1) {
+    hipEvent_t ev;
+    Events E;
+    KP_TRY(E.make(&ev, hipEventDisableTiming));
+    KP_TRY(wait_stream(c, ev));  // a shard polls: a failed peer releases it
+  } else {
+    KP_HIP(hipStreamSynchronize(c->stream));
+  }
+  c->in_collective = false;
   int32_t n_nom = 0;
   for (int32_t j = 0; j < J; ++j) n_nom += nom[j] >= 0;
   out->preemptors = P;

@@ -128,6 +128,7 @@ struct DevState {
   // (node, prio desc, running index asc) with per-node suffix sums, outputs
   int32_t *uprio = nullptr;     // [U]
   int32_t *plist = nullptr;     // [U] preemptor units of the last kp_preempt
+  int32_t *pre_send = nullptr, *pre_recv = nullptr;  // multi-rank preemption blocks
   int32_t *roff = nullptr;      // [N+1]
   int64_t *rreq = nullptr, *rsuf = nullptr;  // [D][R]
   int32_t *rprio = nullptr;     // [R]
@@ -219,6 +220,7 @@ struct kp_ctx {
   int32_t cap_cnt_N = 0;
   // sizes
   int32_t N = 0, D = 0, J = 0, U = 0, R = 0, cap_R = 0, cap_delta = 0;
+  int64_t cap_pre_xg = 0;  // int32 entries of d.pre_send (d.pre_recv: world x that)
   int32_t cap_N = 0, cap_U = 0, cap_J = 0, cap_rows = 0, cap_props = 0, cap_K = 0;
   int32_t mat_Ns = 0;          // row stride the score matrix was allocated for
   int64_t cap_P = 0;           // columns of d.np32
@@ -324,7 +326,12 @@ int launch_finalize(kp_ctx *c);
 int launch_pack_exchange(kp_ctx *c, int32_t B, int32_t K);
 int launch_unpack_exchange(kp_ctx *c, int32_t world, int32_t B, int32_t K);
 size_t rocprim_temp_bytes(int32_t max_items);
-int launch_preempt(kp_ctx *c, int32_t *P_host);
+// preemptor compaction + the scoring of this rank's rows [*lo, *hi) of them
+int launch_preempt(kp_ctx *c, int32_t *P_host, int32_t *lo, int32_t *hi);
+// multi-rank preemption: this rank's rows -> blocks of 4 int32 per row, and
+// every rank's blocks (B rows each) -> the preemptors' jobs
+int launch_preempt_pack(kp_ctx *c, int32_t lo, int32_t hi, int32_t *send);
+int launch_preempt_unpack(kp_ctx *c, int32_t P, int32_t B, const int32_t *recv);
 int launch_delta(kp_ctx *c, int32_t K, int32_t *bad_host);
 
 // context over one GPU (kp_api.cpp); nccl_comm, if given, is adopted

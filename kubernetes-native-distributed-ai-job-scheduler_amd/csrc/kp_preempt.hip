@@ -309,20 +309,21 @@ __global__ void k_preempt_init(int32_t J, int32_t *__restrict__ node, int32_t *_
 
 template <int D>
 struct PreemptL {
-  static int run(kp_ctx *c, int32_t P) {
+  static int run(kp_ctx *c, int32_t lo, int32_t P) {  // preemptor rows [lo, lo + P)
+    const int32_t *plist = c->d.plist + lo;
     // the tiled kernel sums free capacity and evictable requests in u32: after
     // kp_apply_delta lowers usage below the running jobs' sum, that sum can
     // reach ~2 x cap, so it needs every cap < 2^31
     if (c->fits32 && c->preempt32 && c->pre_key_ok && c->max_cap < ((int64_t)1 << 31)) {
       hipLaunchKernelGGL((k_preempt_t<D>), dim3(blocks(P, kPtRows)), dim3(256), 0, c->stream, c->N,
-                         c->U, P, c->R, c->d.plist, c->d.q, c->d.uprio, c->d.leader, c->d.cap,
+                         c->U, P, c->R, plist, c->d.q, c->d.uprio, c->d.leader, c->d.cap,
                          c->d.used, c->d.roff, c->d.rreq, c->d.rsuf, c->d.rprio, c->d.pre_node,
                          c->d.pre_vict, c->d.pre_cost);
       KP_HIP(hipGetLastError());
       return KP_OK;
     }
     hipLaunchKernelGGL((k_preempt<D>), dim3(blocks(P, kPreRows)), dim3(256), 0, c->stream, c->N,
-                       c->U, P, c->R, c->d.plist, c->d.q, c->d.uprio, c->d.leader, c->d.cap,
+                       c->U, P, c->R, plist, c->d.q, c->d.uprio, c->d.leader, c->d.cap,
                        c->d.used, c->d.roff, c->d.rreq, c->d.rsuf, c->d.rprio, c->d.pre_node,
                        c->d.pre_vict, c->d.pre_cost);
     KP_HIP(hipGetLastError());
@@ -330,11 +331,50 @@ struct PreemptL {
   }
 };
 
+// Multi-rank preemption: rank r scores the preemptor rows [lo_r, hi_r) of the
+// (replicated) preemptor list; the per-row results travel as fixed blocks of
+// B = ceil(P / world) rows x {node, victims, cost lo, cost hi} through one
+// all-gather, and every rank scatters all of them to the preemptors' jobs.
+__global__ void k_preempt_pack(int32_t lo, int32_t hi, const int32_t *__restrict__ plist,
+                               const int32_t *__restrict__ leader,
+                               const int32_t *__restrict__ node, const int32_t *__restrict__ vict,
+                               const int64_t *__restrict__ cost, int32_t *__restrict__ send) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lo + i >= hi) return;
+  const int32_t j = leader[plist[lo + i]];
+  const uint64_t cu = (uint64_t)cost[j];
+  send[4 * i] = node[j];
+  send[4 * i + 1] = vict[j];
+  send[4 * i + 2] = (int32_t)(uint32_t)cu;
+  send[4 * i + 3] = (int32_t)(uint32_t)(cu >> 32);
+}
+
+__global__ void k_preempt_unpack(int32_t P, int32_t world, int32_t B,
+                                 const int32_t *__restrict__ plist,
+                                 const int32_t *__restrict__ leader,
+                                 const int32_t *__restrict__ recv, int32_t *__restrict__ node,
+                                 int32_t *__restrict__ vict, int64_t *__restrict__ cost) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;  // preemptor row
+  if (r >= P) return;
+  // owner rank w of row r: lo_w = floor(P w / world) <= r < lo_{w+1}
+  int w = (int)(((int64_t)r * world) / P);
+  while (w + 1 < world && ((int64_t)P * (w + 1)) / world <= r) ++w;
+  while (w > 0 && ((int64_t)P * w) / world > r) --w;
+  const int32_t lo = (int32_t)(((int64_t)P * w) / world);
+  const int32_t *x = recv + ((int64_t)w * B + (r - lo)) * 4;
+  const int32_t j = leader[plist[r]];
+  node[j] = x[0];
+  vict[j] = x[1];
+  cost[j] = (int64_t)(((uint64_t)(uint32_t)x[3] << 32) | (uint32_t)x[2]);
+}
+
 }  // namespace
 
-// preemptor compaction (NO_FIT singletons, rank order) -> count to host
-int launch_preempt(kp_ctx *c, int32_t *P_host) {
+// preemptor compaction (NO_FIT singletons, rank order) -> count to host; the
+// scoring of this rank's rows [*lo, *hi) (all of them on one rank)
+int launch_preempt(kp_ctx *c, int32_t *P_host, int32_t *lo, int32_t *hi) {
   *P_host = 0;
+  *lo = *hi = 0;
   const int32_t U = c->U, J = c->J;
   if (J > 0) {
     hipLaunchKernelGGL(k_preempt_init, dim3(blocks(J, 256)), dim3(256), 0, c->stream, J,
@@ -353,8 +393,29 @@ int launch_preempt(kp_ctx *c, int32_t *P_host) {
   KP_HIP(hipStreamSynchronize(c->stream));
   const int32_t P = c->pinned[0];
   *P_host = P;
-  if (P == 0 || c->N == 0) return KP_OK;
-  return dispatch_D<PreemptL>(c->D, c, P);
+  *lo = (int32_t)(((int64_t)P * c->rank) / c->world);
+  *hi = (int32_t)(((int64_t)P * (c->rank + 1)) / c->world);
+  if (*hi == *lo || c->N == 0) return KP_OK;
+  return dispatch_D<PreemptL>(c->D, c, *lo, *hi - *lo);
+}
+
+int launch_preempt_pack(kp_ctx *c, int32_t lo, int32_t hi, int32_t *send) {
+  if (hi > lo) {
+    hipLaunchKernelGGL(k_preempt_pack, dim3(blocks(hi - lo, 256)), dim3(256), 0, c->stream, lo, hi,
+                       c->d.plist, c->d.leader, c->d.pre_node, c->d.pre_vict, c->d.pre_cost, send);
+    KP_HIP(hipGetLastError());
+  }
+  return KP_OK;
+}
+
+int launch_preempt_unpack(kp_ctx *c, int32_t P, int32_t B, const int32_t *recv) {
+  if (P > 0) {
+    hipLaunchKernelGGL(k_preempt_unpack, dim3(blocks(P, 256)), dim3(256), 0, c->stream, P, c->world,
+                       B, c->d.plist, c->d.leader, recv, c->d.pre_node, c->d.pre_vict,
+                       c->d.pre_cost);
+    KP_HIP(hipGetLastError());
+  }
+  return KP_OK;
 }
 
 }  // namespace kp

@@ -98,3 +98,79 @@ def test_sharded_gpu_solve_matches_oracle(oracle, world, cfg, mpm):
     ok, r1, r0, p1, p0 = res
     assert ok, "sharded GPU placement differs from the oracle"
     assert (r1, p1) == (r0, p0)
+
+
+def _worker_c4(rank, world, port, J, N, out_q):
+    """Config #4 placement + preemption per rank, host-staged exchange: the
+    preemptor rows are split over the ranks and all-gathered."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.join(os.path.dirname(here),
+                                    "kubernetes-native-distributed-ai-job-scheduler_amd"))
+    import torch
+    import oracle_bind as ob
+    from kplace import _abi, synth
+    from kplace.engine import Placer
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def allgather(data: bytes) -> bytes:
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+        bufs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(bufs, t)
+        return b"".join(b.numpy().tobytes() for b in bufs)
+
+    w = synth.config4(J, N)
+    m = w.meta
+    p = _abi.default_params(**synth.CONFIG_PARAMS[4])
+    with Placer(device=0, world_size=world, rank=rank, allgather=allgather) as pl:
+        pl.load_nodes(w.cap, w.used, w.topo)
+        pl.load_running(m["run_node"], m["run_req"], m["run_prio"])
+        pl.load_jobs(w.req, w.prio, w.gang_id, w.gang_size)
+        pl.solve(p)
+        g = pl.fetch()
+        pr = pl.preempt()
+    if rank == 0:
+        ref, rpr = ob.preempt(ob.SnapshotBuf.from_workload(w), p, m["run_node"], m["run_req"],
+                              m["run_prio"], nthreads=8)
+        ok = all(np.array_equal(g[k], ref[k]) for k in ("node", "score", "status", "used"))
+        ok = ok and all(np.array_equal(pr[k], rpr[k]) for k in ("node", "victims", "cost"))
+        ok = ok and pr["nominated"] == rpr["nominated"] and rpr["nominated"] > 0
+        out_q.put((ok, g["rounds"], ref["rounds"], g["placed"], ref["placed"]))
+    out_q.put(("nodes", pr["node"].tolist()))  # every rank holds every nomination
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_gpu_config4_preempt_matches_oracle(oracle, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_c4, args=(r, world, port, 20_000, 2_000, q))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    import queue
+    got = []
+    for _ in range(300):
+        try:
+            got.append(q.get(timeout=1))
+            if len(got) == world + 1:
+                break
+        except queue.Empty:
+            if any(pr.exitcode not in (None, 0) for pr in procs):
+                break
+    for pr in procs:
+        pr.join(timeout=60)
+        if pr.is_alive():
+            pr.kill()
+    assert len(got) == world + 1, f"a rank failed: exit codes {[pr.exitcode for pr in procs]}"
+    res = [x for x in got if x[0] != "nodes"][0]
+    others = [x[1] for x in got if x[0] == "nodes"]
+    ok, r1, r0, p1, p0 = res
+    assert ok, "sharded GPU placement / preemption differs from the oracle"
+    assert (r1, p1) == (r0, p0)
+    assert len(others) == world and all(o == others[0] for o in others)

@@ -971,3 +971,47 @@ def test_fused_key_collisions(oracle, monkeypatch, tie, bits, K):
         assert pl.timing()["fused"] == 1
     o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
     _assert_same(g, o, f"collisions tie={tie} bits={bits} K={K}")
+
+
+# ---------------------------------------------------------------------------
+# the product is the default path: knobs need the gate, fixtures hold on the GPU
+# ---------------------------------------------------------------------------
+def test_knobs_ignored_without_debug_gate(oracle, monkeypatch):
+    """A manager process's inherited environment cannot switch kernels or key
+    encodings: without KP_DEBUG_KNOBS=1, KP_FUSED=0 and KP_FZ_TIE_BITS=1 are
+    ignored at kp_create, so the solve runs the fused candidate phase with the
+    full tie-key width and returns the oracle's placement."""
+    monkeypatch.delenv("KP_DEBUG_KNOBS", raising=False)
+    monkeypatch.setenv("KP_FUSED", "0")
+    monkeypatch.setenv("KP_FZ_TIE_BITS", "1")
+    monkeypatch.setenv("KP_ACC_BIG_RATIO", "1")
+    w = synth.config3(8_000, 800)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[3])
+    with Placer(device=0) as pl:
+        pl.set_profiling(True)
+        g = pl.place(w, p)
+        assert pl.timing()["fused"] == 1, "KP_FUSED=0 honoured without the KP_DEBUG_KNOBS gate"
+    _assert_same(g, oracle.place(_snap(oracle, w), p, nthreads=NTH), "knobs without the gate")
+
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("name", sorted(f for f in os.listdir(GOLDEN) if f.startswith("place_")
+                                        and f.endswith(".npz")))
+def test_golden_fixture_gpu(name):
+    """Every committed golden vector (tests/golden/make_golden.py) fed straight
+    to libkplace: node / score / status / usage and the round and pass counts
+    equal the stored outputs (no oracle in the loop)."""
+    z = np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+    pd = {k[2:]: z[k] for k in z.files if k.startswith("p_")}
+    p = _abi.default_params(**{k: (tuple(int(x) for x in v) if v.ndim else int(v))
+                               for k, v in pd.items()})
+    w = synth.Workload(int(z["req"].shape[1]), int(z["cap"].shape[1]), int(z["req"].shape[0]),
+                       z["req"], z["cap"], z["used"], z["prio"], z["gang_id"], z["gang_size"],
+                       z["topo"], affinity=z["affinity"] if "affinity" in z.files else None)
+    with Placer(device=0) as pl:
+        g = pl.place(w, p)
+    for k in ("node", "score", "status", "used"):
+        assert np.array_equal(g[k], z["out_" + k]), f"{name}: {k}"
+    assert g["rounds"] == int(z["out_rounds"]) and g["passes"] == int(z["out_passes"]), name

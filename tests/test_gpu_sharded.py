@@ -104,3 +104,71 @@ def test_create_multi_shard_failure_releases_peers(oracle, monkeypatch, ids, fai
         g = pl.fetch()
     o = oracle.place(oracle.SnapshotBuf.from_workload(w), p, nthreads=NTH)
     _assert_same(g, o, f"after an injected failure of shard {fail_rank}")
+
+
+# ---------------------------------------------------------------------------
+# BASELINE config #4 sharded: placement + preemption over row shards
+# ---------------------------------------------------------------------------
+def _config4(oracle, J=None, N=None):
+    key = ("c4", J, N)
+    if key not in _CACHE:
+        w = synth.config4(J, N) if J else synth.config4()
+        m = w.meta
+        p = _abi.default_params(**synth.CONFIG_PARAMS[4])
+        o = None
+        if J:
+            o = oracle.preempt(oracle.SnapshotBuf.from_workload(w), p, m["run_node"], m["run_req"],
+                               m["run_prio"], nthreads=NTH)
+        _CACHE[key] = (w, p, o)
+    return _CACHE[key]
+
+
+def _solve_preempt(pl, w, p):
+    m = w.meta
+    pl.load_nodes(w.cap, w.used, w.topo)
+    pl.load_running(m["run_node"], m["run_req"], m["run_prio"])
+    pl.load_jobs(w.req, w.prio, w.gang_id, w.gang_size)
+    st = pl.solve(p)
+    return st, pl.fetch(), pl.preempt()
+
+
+@pytest.mark.parametrize("shards", [2, 4])
+def test_config4_sharded_parity(oracle, shards):
+    """kp_create_multi([0] * G) on config #4's shape (20k x 2k, 30 % occupancy):
+    the candidate phase row-sharded with one exchange per round, and the
+    preemption scoring row-sharded too (shard r scores preemptors
+    [P r / G, P (r + 1) / G), one all-gather of the nominations). Placement,
+    counts and every nomination equal the oracle's."""
+    w, p, (o, opr) = _config4(oracle, 20_000, 2_000)
+    with Placer(gpu_ids=[0] * shards) as pl:
+        st, g, pr = _solve_preempt(pl, w, p)
+    _assert_same(g, o, f"config4 20k, {shards} shards")
+    for k in ("node", "victims", "cost"):
+        assert np.array_equal(pr[k], opr[k]), f"config4 20k, {shards} shards: preempt {k}"
+    for k in ("preemptors", "nominated", "pairs"):
+        assert pr[k] == opr[k], (k, pr[k], opr[k])
+    assert opr["nominated"] > 0
+
+
+@pytest.mark.parametrize("shards", [2, 4])
+def test_config4_full_size_sharded_digests(shards):
+    """Config #4 at BASELINE size (200k x 20k) over 2 and 4 in-process shards:
+    the same digests as the one-GPU run (tests/golden/large_digests.json)."""
+    import hashlib
+    import json
+
+    gold = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                       "large_digests.json")))["config4"]
+
+    def digest(a):
+        a = np.ascontiguousarray(a)
+        return hashlib.sha256(a.astype(a.dtype.newbyteorder("<")).tobytes()).hexdigest()
+
+    w = synth.config4()
+    p = _abi.default_params(**synth.CONFIG_PARAMS[4])
+    with Placer(gpu_ids=[0] * shards) as pl:
+        st, g, pr = _solve_preempt(pl, w, p)
+    assert {k: digest(g[k]) for k in ("node", "score", "status", "used")} == gold["place"]
+    assert {k: digest(pr[k]) for k in ("node", "victims", "cost")} == gold["preempt"]
+    assert {k: int(g[k]) for k in gold["counts"]} == gold["counts"]
+    assert {k: int(pr[k]) for k in gold["preempt_counts"]} == gold["preempt_counts"]
