@@ -396,10 +396,18 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
   st->pairs += (int64_t)active0 * N;
 
   const char *trace_env = getenv("KPO_TRACE"); /* per-round counts on stderr (analysis) */
-  const int trace = trace_env ? (atoi(trace_env) > 1 ? 2 : 1) : 0;
+  const int trace = trace_env ? (atoi(trace_env) > 2 ? 3 : atoi(trace_env) > 1 ? 2 : 1) : 0;
   int32_t passes0 = st->passes;
+  /* KPO_DUMP=path (analysis, tools/accept_sim.py): per round the candidates,
+     per pass the proposals with their first-fit outcome, appended as int32 */
+  FILE *dump = getenv("KPO_DUMP") ? fopen(getenv("KPO_DUMP"), "ab") : NULL;
+  if (dump) {
+    int32_t h[4] = {-1, st->rounds, U, K};
+    fwrite(h, sizeof h, 1, dump);
+    fwrite(cand, sizeof(int32_t), (size_t)U * K, dump);
+  }
   int32_t *chg_pass = NULL; /* KPO_TRACE=2 analysis: last pass that changed each node's usage */
-  if (trace > 1) {
+  if (trace == 2) {
     chg_pass = (int32_t *)malloc(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
     for (int32_t n = 0; chg_pass && n < N; ++n) chg_pass[n] = -2;
   }
@@ -437,6 +445,7 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
     }
     /* per node, in unit rank order: first-fit against the remaining capacity */
     int64_t rem[KP_MAX_DIMS];
+    int32_t tr_maxrow = 0, tr_maxlast = 0, tr_maxsuf = 0; /* KPO_TRACE=3 (analysis) */
     for (int32_t i = 0; i < np;) {
       int32_t node = props[i].node, e = i;
       while (e < np && props[e].node == node) ++e;
@@ -452,7 +461,45 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
         if (fits)
           for (int d = 0; d < D; ++d) rem[d] -= (int64_t)props[k].count * q[d];
       }
+      if (trace > 2) {
+        /* bids of the row; index of its last accepted bid; bids walked until the
+           remaining capacity is below the smallest later request in some dim */
+        int32_t last = -1, suf = e - i;
+        for (int32_t k = i; k < e; ++k) if (ok[k]) last = k - i;
+        int64_t r2[KP_MAX_DIMS];
+        for (int d = 0; d < D; ++d) r2[d] = st->cap[(int64_t)d * N + node] - st->used[(int64_t)d * N + node];
+        for (int32_t k = i; k < e; ++k) {
+          int64_t q[KP_MAX_DIMS];
+          unit_req(st, props[k].unit, q);
+          if (ok[k]) for (int d = 0; d < D; ++d) r2[d] -= (int64_t)props[k].count * q[d];
+          int stop = 0;
+          for (int d = 0; d < D && !stop; ++d) {
+            int64_t mn = INT64_MAX;
+            for (int32_t k2 = k + 1; k2 < e; ++k2) {
+              int64_t q2[KP_MAX_DIMS];
+              unit_req(st, props[k2].unit, q2);
+              if (q2[d] < mn) mn = q2[d];
+            }
+            if (k + 1 < e && r2[d] < mn) stop = 1;
+          }
+          if (stop) { suf = k + 1 - i; break; }
+        }
+        if (e - i > tr_maxrow) tr_maxrow = e - i;
+        if (last + 1 > tr_maxlast) tr_maxlast = last + 1;
+        if (suf > tr_maxsuf) tr_maxsuf = suf;
+      }
       i = e;
+    }
+    if (trace > 2)
+      fprintf(stderr, "kpo accept %d.%d maxrow %d maxlast %d maxsuf %d\n", st->rounds, pass, tr_maxrow,
+              tr_maxlast, tr_maxsuf);
+    if (dump) {
+      int32_t h[4] = {-2, pass, np, 0};
+      fwrite(h, sizeof h, 1, dump);
+      for (int32_t k = 0; k < np; ++k) {
+        int32_t r[4] = {props[k].unit, props[k].node, props[k].count, ok[k]};
+        fwrite(r, sizeof r, 1, dump);
+      }
     }
     /* all-or-nothing: a unit is placed iff every proposal was accepted */
     for (int32_t k = 0; k < np; ++k) gang_bad[props[k].unit] = 0;
@@ -477,6 +524,7 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
   if (trace)
     fprintf(stderr, "kpo round %d active %d passes %d\n", st->rounds, active0, st->passes - passes0);
   st->rounds++;
+  if (dump) fclose(dump);
   free(chg_pass);
   free(open); free(props); free(ok); free(gang_bad);
   return kpo_state_active(st);
