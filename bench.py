@@ -266,6 +266,43 @@ def config4(args, make_placer):
             "preempt_pairs": pr["pairs"], "steps": args.c4_steps}
 
 
+def score_matrix(args, make_placer, w, p):
+    """The materialised filter + score outputs north_star names (int32 score
+    matrix + feasibility bitmask) for the WHOLE config #3 queue, written into
+    HBM by kp_score_dev (k_score32's capacity-class form): HIP-event kernel
+    time and algorithmic bytes (outputs once + requests + node planes) from
+    kp_last_timing, against the HBM peak."""
+    from kplace.devmem import DeviceBuffer  # libkplace's own HIP runtime (not torch's)
+    Ns = (w.N + 63) // 64 * 64
+    sc = DeviceBuffer(w.J * Ns * 4)
+    mk = DeviceBuffer(w.J * (Ns // 64) * 8)
+    ms, by, ln, tm = 0.0, 0, 0, None
+    with make_placer() as pl:
+        pl.load_nodes(w.cap, w.used, w.topo)
+        pl.load_jobs(w.req, w.prio, w.gang_id, w.gang_size)
+        pl.set_profiling(True)
+        for it in range(args.score_steps + 1):
+            pl.score_dev(p, 0, w.J, sc.ptr, mk.ptr)
+            tm = pl.timing()
+            if it:  # first call: warmup
+                ms += tm["score_ms"]
+                by += tm["score_bytes"]
+                ln += tm["score_launches"]
+    sc.close()
+    mk.close()
+    gbs = (by / 1e9) / (ms / 1e3) if ms > 0 else 0.0
+    pairs = float(w.J) * w.N * args.score_steps
+    return {"kernel": "k_score32c (capacity-class form)" if tm["score_form"] == 1 else "k_score32",
+            "entry": "kp_score_dev", "rows": w.J, "nodes": w.N, "row_stride": Ns,
+            "capacity_classes": tm["score_classes"], "calls": args.score_steps,
+            "launches_per_call": ln / max(args.score_steps, 1),
+            "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": gbs / HBM_PEAK_GBS, "bytes_per_call": by / max(args.score_steps, 1),
+            "ms_per_call": ms / max(args.score_steps, 1), "pairs_per_s": pairs / (ms / 1e3) if ms else 0.0,
+            "algorithmic_bytes": "rows x Ns x 4 (scores) + rows x Ns / 8 (mask) + rows x (8D + 4) "
+                                 "(requests) + (2D + 4) x 4 x Ns (node planes)"}
+
+
 def relaunch_distributed(args) -> int:
     """`--gpus N` without a launcher: run this script under
     torch.distributed.run as N ranks (a child process; this process never
@@ -308,6 +345,8 @@ def main():
     ap.add_argument("--c4-nodes", type=int, default=20_000)
     ap.add_argument("--c4-steps", type=int, default=3)
     ap.add_argument("--no-config4", action="store_true")
+    ap.add_argument("--no-score-matrix", action="store_true")
+    ap.add_argument("--score-steps", type=int, default=3, help="kp_score_dev calls of the score-matrix leg")
     ap.add_argument("--cpu-c4-jobs", type=int, default=25_000,
                     help="config #4 CPU baseline sample: the first N pending jobs")
     ap.add_argument("--cpu-c4-rounds", type=int, default=3,
@@ -499,6 +538,9 @@ def main():
                      "avg_launch_ms": score_ms / max(launches, 1),
                      "valu": valu},
     }
+    if not args.no_score_matrix and n_gpus == 1:
+        progress("score matrix leg")
+        out["score_matrix"] = score_matrix(args, make_placer, w, p)
     if not args.no_config4 and n_gpus == 1:
         progress("config #4 leg")
         out["config4"] = config4(args, make_placer)

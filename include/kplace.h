@@ -33,7 +33,8 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 5  /* 4: kp_last_error_r; 5: kp_timing.incr_rounds */
+#define KP_ABI_VERSION 6  /* 4: kp_last_error_r; 5: kp_timing.incr_rounds;
+                              6: kp_score_dev, kp_timing.score_form / score_classes */
 
 /* ---- limits ------------------------------------------------------------ */
 #define KP_MAX_DIMS 8       /* resource dimensions per job/node               */
@@ -226,6 +227,19 @@ int kp_score(kp_ctx *ctx, const kp_params *p, int32_t job_lo, int32_t job_hi,
              int32_t *score, uint64_t *mask);
 
 /*
+ * The same filter + score pass into DEVICE memory that the caller owns on the
+ * context's GPU (e.g. a consumer that keeps the matrix in HBM for its own
+ * kernels): rows [job_lo, job_hi) with the padded row stride Ns =
+ * round_up(N, 64): score_dev[(j-job_lo)*Ns + n] (padding columns
+ * KP_SCORE_INFEASIBLE) and mask_dev[(j-job_lo)*(Ns/64) + n/64]. Either may be
+ * NULL. Complete on return; with kp_set_profiling on, kp_last_timing reports
+ * the kernels' HIP-event time (score_ms) and algorithmic bytes (score_bytes).
+ * Not available on a kp_create_multi context (KP_EINVAL).
+ */
+int kp_score_dev(kp_ctx *ctx, const kp_params *p, int32_t job_lo, int32_t job_hi,
+                 int32_t *score_dev, uint64_t *mask_dev);
+
+/*
  * Preemption candidates (BASELINE config #4).
  *
  * The running jobs of the resident node table form the victim pool: running
@@ -271,9 +285,11 @@ typedef struct kp_timing {
   int64_t select_bytes;     /* algorithmic bytes of the select kernels       */
   int32_t fused;            /* 1: fused filter+score+top-K (no score matrix;
                                score_* then time/count k_score_topk)         */
-  int32_t loop_rounds;      /* rounds whose passes ran as one persistent launch */
-  int32_t incr_rounds;      /* rounds whose candidates came from the incremental
-                               update (score_* then cover the full scans only) */
+  int32_t score_form;       /* kp_score / kp_score_dev / the materialised solve
+                               path: 1 = the capacity-class form (k_score32c),
+                               0 = the per-wave uniform / mixed form */
+  int32_t score_classes;    /* capacity classes of the node table (0: more than
+                               the class form handles) */
   int32_t pad;
 } kp_timing;
 int kp_last_timing(kp_ctx *ctx, kp_timing *t);

@@ -131,6 +131,8 @@ static int ensure_nodes(kp_ctx *c, int32_t N, int32_t D) {
   KP_TRY(dalloc(&c->d.nrec, (size_t)n + 16));
   KP_TRY(dalloc(&c->d.nst, (size_t)n * 16));
   KP_TRY(dalloc(&c->d.perm, (size_t)n));
+  KP_TRY(dalloc(&c->d.ncls, (size_t)n));
+  KP_TRY(dalloc(&c->d.ccap, (size_t)kScoreClasses * KP_MAX_DIMS));
   c->cap_N = n;
   return KP_OK;
 }
@@ -138,7 +140,7 @@ static int ensure_nodes(kp_ctx *c, int32_t N, int32_t D) {
 // 32-bit node planes: [5*D+3][cols], cols = the widest layout in use (the
 // fused solve's class-aligned columns or round_up(N, 1024))
 static int ensure_np32(kp_ctx *c, int64_t cols, int32_t D) {
-  const int64_t need = (int64_t)(5 * D + 3) * std::max<int64_t>(cols, 1024);
+  const int64_t need = (int64_t)(5 * D + 4) * std::max<int64_t>(cols, 1024);
   if (c->d.np32 && need <= c->cap_P) return KP_OK;
   c->cap_P = 0;
   KP_TRY(dalloc(&c->d.np32, (size_t)need));
@@ -175,6 +177,7 @@ static int ensure_units(kp_ctx *c, int32_t U, int32_t J) {
     KP_TRY(dalloc(&c->d.gpart, pm));
     KP_TRY(dalloc(&c->d.win, pm / 64 + 128));
     KP_TRY(dalloc(&c->d.winmin, (pm / 64 + 128) * KP_MAX_DIMS));
+    KP_TRY(dalloc(&c->d.bmin, (pm / 64 + 128) * KP_MAX_DIMS));
     KP_TRY(dalloc(&c->d.nparts, u));
     KP_TRY(dalloc(&c->d.arrive, u));
     KP_TRY(dalloc(&c->d.uprio, u));
@@ -333,9 +336,11 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = knob("KP_SCORE_NPL")) c->score_npl = std::atoi(e) == 4 ? 4 : 2;
   if (const char *e = knob("KP_COMPACT_MAX")) c->compact_max = std::atoi(e);
   if (const char *e = knob("KP_FUSED")) c->fused_enabled = std::atoi(e) != 0;
+  if (const char *e = knob("KP_SCORE_CLASSES")) c->score_classes = std::atoi(e) != 0;
   if (const char *e = knob("KP_PREEMPT32")) c->preempt32 = std::atoi(e) != 0;
   if (const char *e = knob("KP_ACC_LIST")) c->acc_list = std::atoi(e);
   if (const char *e = knob("KP_ACC_BIG_RATIO")) c->acc_big_ratio = std::max(0, std::atoi(e));
+  if (const char *e = knob("KP_BMIN_WIN")) c->bmin_windows = std::max(1, std::atoi(e));
   if (const char *e = knob("KP_PASS_FOLLOW")) c->pass_follow = std::max(0, std::min(64, std::atoi(e)));
   if (const char *e = knob("KP_KEYS_MERGE")) c->keys_merge_enabled = std::atoi(e) != 0;
   if (const char *e = knob("KP_ROUND_BEGIN")) c->round_begin = std::atoi(e) != 0;
@@ -463,6 +468,34 @@ static int load_nodes_impl(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap,
     return fail(KP_ENOMEM, "kp_load_nodes: host copy");
   }
   const int32_t fz_P = (int32_t)colnode.size();
+  // capacity classes for k_score32's class form: the runs of equal capacity
+  // vectors in canonical order (at most kScoreClasses of them)
+  std::vector<uint32_t> ncls, ccap;
+  int32_t n_classes = 0;
+  try {
+    int32_t k = 0;
+    for (int32_t i = 0; i < N && k <= kScoreClasses; ++k) {
+      int32_t e = i + 1;
+      while (e < N && [&] {
+        for (int d = 0; d < D; ++d)
+          if (cap[(int64_t)d * N + c->h_perm[e]] != cap[(int64_t)d * N + c->h_perm[i]]) return false;
+        return true;
+      }()) ++e;
+      if (k < kScoreClasses) {
+        if (ncls.empty()) {
+          ncls.assign((size_t)N, 0u);
+          ccap.assign((size_t)kScoreClasses * D, 0u);
+        }
+        for (int32_t j = i; j < e; ++j) ncls[(size_t)c->h_perm[j]] = (uint32_t)k;
+        for (int d = 0; d < D; ++d) ccap[(size_t)k * D + d] = (uint32_t)cap[(int64_t)d * N + c->h_perm[i]];
+      }
+      i = e;
+      if (i >= N) n_classes = k + 1;
+    }
+    if (n_classes > kScoreClasses) n_classes = 0;
+  } catch (const std::bad_alloc &) {
+    return fail(KP_ENOMEM, "kp_load_nodes: host copy");
+  }
   KP_TRY(ensure_nodes(c, N, D));
   KP_TRY(ensure_np32(c, std::max<int64_t>(fz_P, ((int64_t)N + 1023) & ~(int64_t)1023), D));
   if (fz_P > 0) {
@@ -488,6 +521,12 @@ static int load_nodes_impl(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap,
                           hipMemcpyHostToDevice, c->stream));
     KP_HIP(hipMemcpyAsync(c->d.perm, c->h_perm.data(), sizeof(int32_t) * N,
                           hipMemcpyHostToDevice, c->stream));
+    if (n_classes > 0) {
+      KP_HIP(hipMemcpyAsync(c->d.ncls, ncls.data(), sizeof(uint32_t) * N, hipMemcpyHostToDevice,
+                            c->stream));
+      KP_HIP(hipMemcpyAsync(c->d.ccap, ccap.data(), sizeof(uint32_t) * (size_t)n_classes * D,
+                            hipMemcpyHostToDevice, c->stream));
+    }
   }
   // the victim pool belongs to the previous node table
   KP_HIP(hipMemsetAsync(c->d.roff, 0, sizeof(int32_t) * ((size_t)N + 1), c->stream));
@@ -502,6 +541,7 @@ static int load_nodes_impl(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap,
   // the fused layout pays off while the padding stays small (few capacity
   // classes); the merge holds at most 2,048 keys per row (tiles x K)
   c->fz_P = fz_P;
+  c->n_classes = (c->max_cap < ((int64_t)1 << 32)) ? n_classes : 0;
   c->fz_layout_ok = fz_P > 0 && fz_cols - N <= N / 8 + 1024;
   c->fits32 = c->caps32 && c->reqs32 && c->jobs_loaded;
   c->util_scale_loaded = 0;  // force a division-table rebuild at the next solve
@@ -757,7 +797,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     const void *need[] = {d.cap, d.used, d.R32, d.K32, d.base, d.topo, d.perm, d.np32, d.q, d.leader,
                           d.size, d.status, d.salt, d.aff, d.job_node, d.job_score, d.job_status,
                           d.act, d.act_local, d.cand, d.cand_local, d.open, d.flag, d.s0, d.bid,
-                          d.win, d.winmin, d.gpart, d.nparts, d.arrive, d.inv, d.ent_unit,
+                          d.win, d.winmin, d.bmin, d.gpart, d.nparts, d.arrive, d.inv, d.ent_unit,
                           d.ent_slot, d.ent_size, d.ent_lead, d.ent_q, d.csr_kin, d.csr_vin,
                           d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.node_flag, d.node_list, d.nrec, d.nst,
                           d.pass_flag, d.counters, d.stats, d.temp};
@@ -1094,6 +1134,8 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   }
   tm.accept_ms = tm.solve_ms - tm.score_ms - tm.select_ms;
   tm.fused = fused ? 1 : 0;
+  tm.score_classes = c->n_classes;
+  tm.score_form = !fused && c->fits32 && c->n_classes > 0 && c->score_classes ? 1 : 0;
   c->timing = tm;
   int32_t placed = 0;
   for (int32_t u = 0; u < U; ++u)
@@ -1279,15 +1321,15 @@ void kp_destroy(kp_ctx *c) {
   void *ptrs[] = {d.cap, d.used, d.used0, d.R32, d.K32, d.base, d.topo, d.q, d.leader, d.size,
                   d.status, d.salt, d.aff,
                   d.job_node, d.job_score, d.job_status, d.act_local, d.cand_local, d.score,
-                  d.mask, d.open, d.flag, d.s0, d.bid, d.gpart, d.nparts, d.arrive, d.win, d.winmin,
+                  d.mask, d.open, d.flag, d.s0, d.bid, d.gpart, d.nparts, d.arrive, d.win, d.winmin, d.bmin,
                   d.inv, d.ent_unit,
                   d.ent_slot, d.ent_size, d.ent_lead, d.ent_q, d.perm,
                   d.csr_kin, d.csr_vin,
                   d.csr_keys, d.csr_vals, d.seg_start, d.seg_end, d.pass_flag, d.counters,
                   d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.pre_send, d.pre_recv, d.roff,
                   d.rreq, d.rsuf, d.rprio, d.pre_node, d.pre_vict, d.pre_cost,
-                  d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.nrec, d.nst, d.stats, d.np32, d.colnode, d.wshift, d.part, d.fz_prof,
-                  d.bm, d.rowinfo, d.cnt};
+                  d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.nrec, d.nst, d.stats, d.np32, d.ncls, d.ccap, d.colnode, d.wshift, d.part, d.fz_prof,
+                  d.bm, d.bms, d.rowinfo, d.cnt};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->world > 1) {
@@ -1489,6 +1531,73 @@ int kp_score(kp_ctx *c, const kp_params *p, int32_t job_lo, int32_t job_hi, int3
       if (mask) std::memcpy(mask + (r0 + r) * uw, hm.data() + (size_t)r * words, sizeof(uint64_t) * uw);
     }
   }
+  return KP_OK;
+}
+
+int kp_score_dev(kp_ctx *c, const kp_params *p, int32_t job_lo, int32_t job_hi,
+                 int32_t *score_dev, uint64_t *mask_dev) {
+  if (!c) return KP_EINVAL;
+  if (c->multi) {
+    std::lock_guard<std::mutex> g(c->mu);
+    c->last_error = "kp_score_dev: not available on a kp_create_multi context";
+    return KP_EINVAL;
+  }
+  Entry en(c);
+  if (!c->nodes_loaded || !c->jobs_loaded)
+    return fail(KP_ESTATE, "kp_score_dev: load nodes and jobs first");
+  KP_TRY(check_params(p, c->D));
+  if (job_lo < 0 || job_hi > c->J || job_lo > job_hi)
+    return fail(KP_EINVAL, "kp_score_dev: job range [%d, %d) of %d", job_lo, job_hi, c->J);
+  KP_HIP(hipSetDevice(c->device));
+  const int32_t rows = job_hi - job_lo, N = c->N, D = c->D;
+  kp_timing tm{};
+  tm.score_classes = c->n_classes;
+  tm.score_form = c->fits32 && c->n_classes > 0 && c->score_classes ? 1 : 0;
+  c->timing = tm;
+  if (rows == 0 || N == 0) return KP_OK;
+  KP_TRY(prep_for(c, p));
+  const ScoreParams sp = make_sp(c, p);
+  const int64_t Ns = (N + 63) & ~63, words = Ns / 64;
+  // job -> unit (rank position) of every requested row, staged in chunks of
+  // at most cap_U rows through act_local
+  std::vector<int32_t> unit_of(rows);
+  {
+    std::vector<int32_t> u_of_job(c->J);
+    for (int32_t u = 0; u < c->U; ++u)
+      for (int32_t m = 0; m < c->h_size[u]; ++m) u_of_job[c->h_leader[u] + m] = u;
+    for (int32_t r = 0; r < rows; ++r) unit_of[r] = u_of_job[job_lo + r];
+  }
+  c->pack_sp = sp;
+  c->pack_canonical = false;  // node order
+  c->pack_fused = false;
+  c->pack_full = true;
+  KP_TRY(launch_pack(c));
+  Events E;
+  const int64_t chunk = std::max<int32_t>(c->cap_U, 1);
+  for (int64_t r0 = 0; r0 < rows; r0 += chunk) {
+    const int32_t nr = (int32_t)std::min<int64_t>(chunk, rows - r0);
+    KP_HIP(hipMemcpyAsync(c->d.act_local, unit_of.data() + r0, sizeof(int32_t) * nr,
+                          hipMemcpyHostToDevice, c->stream));
+    hipEvent_t a = nullptr, b = nullptr;
+    if (c->profiling) {
+      KP_TRY(E.make(&a, hipEventDisableSystemFence));
+      KP_TRY(E.make(&b, hipEventDisableSystemFence));
+      KP_HIP(hipEventRecord(a, c->stream));
+    }
+    KP_TRY(launch_score(c, sp, c->d.act_local, nr, score_dev ? score_dev + r0 * Ns : nullptr,
+                        mask_dev ? mask_dev + r0 * words : nullptr, c->d.q, c->U));
+    if (c->profiling) {
+      KP_HIP(hipEventRecord(b, c->stream));
+      KP_HIP(hipEventSynchronize(b));
+      c->timing.score_ms += ev_ms(a, b);
+    }
+    // algorithmic bytes: the outputs written once, each row's request and the
+    // node planes (free, a per dim; base, topo, WA, class) read once
+    c->timing.score_bytes += (score_dev ? (int64_t)nr * Ns * 4 : 0) + (mask_dev ? (int64_t)nr * words * 8 : 0) +
+                             (int64_t)nr * (8 * D + 4) + (int64_t)(2 * D + 4) * 4 * Ns;
+    c->timing.score_launches++;
+  }
+  KP_HIP(hipStreamSynchronize(c->stream));
   return KP_OK;
 }
 

@@ -453,7 +453,7 @@ __device__ __forceinline__ int mbcnt64(uint64_t m) {
 
 // k_csr_keys' per-round state reset, thread t of the extra workgroups of the
 // kernel that opens the round's slots (the candidate merge, rk.enabled): round statistics, the previous round's
-// productive passes, node segments / flags, window flags
+// productive passes, node segments / flags, window flags and bid minima
 __device__ __forceinline__ void round_keys_init(const RoundKeys &rk, int64_t t) {
   if (t == 0) {
     const int32_t Aa = rk.A_dev ? min(rk.A, *rk.A_dev) : rk.A;
@@ -467,7 +467,10 @@ __device__ __forceinline__ void round_keys_init(const RoundKeys &rk, int64_t t) 
     rk.seg_start[t] = -1;
     rk.node_flag[t] = -1;
   }
-  if (t < rk.nwin) rk.win[t] = -1;
+  if (t < rk.nwin) {
+    rk.win[t] = -1;
+    for (int d = 0; d < rk.D; ++d) rk.bmin[(int64_t)d * rk.nwin + t] = 0;  // no bid yet
+  }
   if (t < 64) {
     if (rk.pass_flag[t] != 0)
       atomicAdd(reinterpret_cast<unsigned long long *>(&rk.st->passes), 1ull);
@@ -482,7 +485,10 @@ __device__ __forceinline__ void round_keys_slot(const RoundKeys &rk, int32_t slo
                                                 int32_t K, int32_t node, int lane) {
   if (lane < K) {
     rk.bid[(int64_t)slot * K + lane] = 0xFFFFFFFFu;  // kNoBid
-    if (node >= 0) atomicOr(&rk.bm[(int64_t)node * rk.Wb + (slot >> 5)], 1u << (slot & 31));
+    // the first bit of a word also sets the word's summary bit
+    if (node >= 0 &&
+        atomicOr(&rk.bm[(int64_t)node * rk.Wb + (slot >> 5)], 1u << (slot & 31)) == 0u)
+      atomicOr(&rk.bms[(int64_t)node * rk.Ws + (slot >> 10)], 1u << ((slot >> 5) & 31));
   }
   const int32_t first = __shfl(node, 0, 64);
   if (lane == 0) {

@@ -28,6 +28,10 @@ static_assert(kTieMul * kTieMulInv == 1u, "tie multiplier must be invertible");
 
 enum UnitStatus : int32_t { kActive = 0, kPlaced = 1, kNoFit = 2 };
 
+// k_score32's class form (kp_score.hip): node tables with at most this many
+// distinct capacity vectors get per-(row, class) thresholds staged in LDS
+constexpr int kScoreClasses = 8;
+
 // d.pass_flag layout: [0, 64) productive-pass flags of the current round
 constexpr int kPassFlagWords = 128;
 // d.counters words: [0] this rank's active units, [1] the global count, [32]
@@ -45,9 +49,11 @@ struct SolveStats {
 // set the slot bitmap bits, re-initialise the pass state (one launch fewer
 // per round). enabled = 0: k_csr_keys runs instead.
 struct RoundKeys {
-  int32_t enabled, A, K, N;
+  int32_t enabled, A, K, N, D;
   int64_t nwin, Wb, init_n;
-  uint32_t *bm, *bid;
+  uint32_t *bm, *bms, *bid;  // bms: one bit per nonzero bm word (Ws words per row)
+  int64_t Ws;
+  int64_t *bmin;
   int32_t *win, *seg_start, *pass_flag, *node_flag, *nl_count, *status;
   uint8_t *open;
   const int32_t *A_dev;
@@ -77,7 +83,11 @@ struct DevState {
   int64_t *base = nullptr;  // LeastAllocated base: sum of w*S over dims with cap > 0
   int32_t *topo = nullptr;
   int32_t *perm = nullptr;  // [N] canonical order: nodes sorted by (cap vector, index)
-  uint32_t *np32 = nullptr;  // [5*D+3][cap_P] 32-bit score tile planes
+  uint32_t *np32 = nullptr;  // [5*D+4][cap_P] 32-bit score tile planes
+  // capacity classes (distinct capacity vectors) when there are at most
+  // kScoreClasses of them: class of each node, and the classes' capacities
+  uint32_t *ncls = nullptr;  // [N]
+  uint32_t *ccap = nullptr;  // [kScoreClasses][D]
   // fused solve layout: canonical order with every capacity
   // class starting on a 128-column wave tile; column -> node (-1 = padding)
   // and per wave tile the canonical position of its first column minus that
@@ -107,8 +117,14 @@ struct DevState {
   // count and an arrival counter (the last accepted part commits the gang)
   int32_t *s0 = nullptr;        // [U*K]
   uint32_t *bid = nullptr;      // [U*K] (pass << 8) | members
-  int32_t *win = nullptr;       // [U*K/64 + 64] last pass with a bid in each 64-entry window
-  int64_t *winmin = nullptr;    // [D][P/64 + 64] smallest request per 64-entry window
+  // per 64-entry bidder window: the last pass with a bid of a short bidder
+  // row in it, the smallest request per dim of its entries (once per round),
+  // and [D][P/64 + 64] the smallest bid (members x request) of the long
+  // rows' bids of the current pass, tagged (pass + 1) << 48 | (2^48 - 1 -
+  // min) by the plan's atomicMax (0 = none this round)
+  int32_t *win = nullptr;       // [P/64 + 128]
+  int64_t *winmin = nullptr;    // [D][P/64 + 64]
+  int64_t *bmin = nullptr;      // [D][P/64 + 64]
   int4 *gpart = nullptr;        // [U*K]
   int32_t *nparts = nullptr;    // [U]
   int32_t *arrive = nullptr;    // [U]
@@ -141,8 +157,10 @@ struct DevState {
   int32_t *counters = nullptr;  // small device counters
   SolveStats *stats = nullptr;  // [1]
   // counting-mode CSR (kp_pass.hip): [N][ceil(A/32)] slot bitmap (all-zero
-  // between rounds), per word {rank of its first bit in the row, bits}, row lengths
+  // between rounds), its summary [N][ceil(A/1024)] (bit w of a row: bm word w
+  // is nonzero), per word {rank of its first bit in the row, bits}, row lengths
   uint32_t *bm = nullptr;
+  uint32_t *bms = nullptr;
   uint2 *rowinfo = nullptr;
   int32_t *cnt = nullptr;
   void *temp = nullptr;         // rocprim temporary storage
@@ -213,9 +231,10 @@ struct kp_ctx {
   // node -> bidder index by counting (KP_CSR_SORT=1: rocprim radix sort)
   bool csr_count_enabled = true, bm_dirty = false;
   int32_t csr_mode = 0;  // the current round's index: 1 counting, 0 sort
-  // counting mode while the round's bitmap (N x ceil(A/32) words) has at most
-  // this many words (KP_CSR_BM_MAX); larger rounds use the radix sort
-  int64_t csr_bm_max = int64_t{1} << 25;
+  // counting mode while the round's bitmap (N x ceil(A/32) words, 12 B each
+  // with its row info) has at most this many words (KP_CSR_BM_MAX, 3 GB);
+  // larger rounds, or a bitmap that cannot be allocated, use the radix sort
+  int64_t csr_bm_max = int64_t{1} << 28;
   int64_t cap_bm_words = 0;
   int32_t cap_cnt_N = 0;
   // sizes
@@ -229,6 +248,8 @@ struct kp_ctx {
   // fused score + top-K (k_score_topk): columns of the class-aligned layout,
   // whether that layout is compact enough to use, KP_FUSED=0 disables it
   int32_t fz_P = 0;
+  int32_t n_classes = 0;  // capacity classes of the node table (0: more than kScoreClasses)
+  bool score_classes = true;  // KP_SCORE_CLASSES=0: k_score32 without the class form
   bool fz_layout_ok = false, fused_enabled = true;
   int64_t max_cap = 0, max_req = 0;  // largest cap / request of the loaded tables
   int32_t cap_mask_rows = 0;   // rows of d.mask (kp_score only)
@@ -255,6 +276,10 @@ struct kp_ctx {
   // the first pass without proposals (0 = every round enqueues max_passes)
   int32_t *hpass = nullptr;
   int32_t pass_follow = 2;
+  // KP_BMIN_WIN: bidder rows spanning at least this many 64-entry windows get
+  // per-pass window bid minima (plan atomics) on top of the round's request
+  // minima; shorter rows only flags
+  int32_t bmin_windows = 64;
   int32_t acc_big_ratio = 48;  // k_accept's long-row form when A*K >= ratio * N (0: never)
   bool hpass_on = false;
   void *stage = nullptr;  // pinned staging of kp_load_jobs' unit arrays
@@ -288,9 +313,12 @@ int launch_pack(kp_ctx *c);
 // Kernels that take a device count pointer (rows_dev / A_dev, nullable) size
 // their grid by the host bound and clamp to the device count, so a round can
 // be enqueued before the host knows its exact number of active units.
+// (sstride / mstride: row strides of score / mask in elements, 0 = the
+// internal layout Ns / Ns / 64; the non-class forms take the internal one only)
 int launch_score(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit,
                  int32_t rows, int32_t *score, uint64_t *mask, const int64_t *q,
-                 int32_t qstride, const int32_t *rows_dev = nullptr);
+                 int32_t qstride, const int32_t *rows_dev = nullptr, int64_t sstride = 0,
+                 int64_t mstride = 0);
 int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit,
                   int32_t rows, const int32_t *score, int32_t *cand,
                   const int32_t *rows_dev = nullptr);

@@ -143,12 +143,14 @@ constexpr uint32_t kNoBid = 0xFFFFFFFFu;  // tag that matches no pass
 __global__ void k_csr_keys(int32_t A, int32_t K, int32_t N, int64_t nwin,
                            const int32_t *__restrict__ cand, uint32_t *__restrict__ keys,
                            uint32_t *__restrict__ vals, uint32_t *__restrict__ bid,
-                           int32_t *__restrict__ win, int32_t *__restrict__ seg_start,
+                           int32_t *__restrict__ win, int64_t *__restrict__ bmin, int32_t D,
+                           int32_t *__restrict__ seg_start,
                            int32_t *__restrict__ pass_flag, int32_t *__restrict__ node_flag,
                            int32_t *__restrict__ nl_count, const int32_t *__restrict__ A_dev,
                            SolveStats *__restrict__ st, const int32_t *__restrict__ act,
                            uint8_t *__restrict__ open, int32_t *__restrict__ status,
-                           uint32_t *__restrict__ bm, int64_t Wb) {
+                           uint32_t *__restrict__ bm, uint32_t *__restrict__ bms, int64_t Wb,
+                           int64_t Ws) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int32_t Aa = A_dev ? min(A, *A_dev) : A;  // slots past the device count: no bids
   if (t == 0 && Aa > 0) {  // one writer: a round with active units
@@ -164,7 +166,9 @@ __global__ void k_csr_keys(int32_t A, int32_t K, int32_t N, int64_t nwin,
     const int32_t n = t < (int64_t)Aa * K ? cand[t] : -1;
     const int32_t a = (int32_t)(t / K), c = (int32_t)(t % K);
     if (bm) {  // counting mode: slot a bids on node n = bit a of row n
-      if (n >= 0) atomicOr(&bm[(int64_t)n * Wb + (a >> 5)], 1u << (a & 31));
+      // the first bit of a word also sets the word's summary bit
+      if (n >= 0 && atomicOr(&bm[(int64_t)n * Wb + (a >> 5)], 1u << (a & 31)) == 0u)
+        atomicOr(&bms[(int64_t)n * Ws + (a >> 10)], 1u << ((a >> 5) & 31));
     } else {
       keys[t] = n >= 0 ? (uint32_t)n : (uint32_t)N;  // invalid entries sort after every node
       vals[t] = ((uint32_t)a << 5) | (uint32_t)c;     // K <= 32
@@ -176,7 +180,10 @@ __global__ void k_csr_keys(int32_t A, int32_t K, int32_t N, int64_t nwin,
     node_flag[t] = -1;
   }
   if (t == 0) *nl_count = 0;
-  if (t < nwin) win[t] = -1;
+  if (t < nwin) {
+    win[t] = -1;
+    for (int d = 0; d < D; ++d) bmin[(int64_t)d * nwin + t] = 0;  // no bid yet
+  }
   if (t < 64) {  // the previous round's productive passes, then clear
     if (pass_flag[t] != 0) atomicAdd(reinterpret_cast<unsigned long long *>(&st->passes), 1ull);
     pass_flag[t] = 0;
@@ -215,7 +222,7 @@ __global__ void k_csr_finish(int32_t P, int32_t N, int32_t K, int32_t D, int32_t
   const uint32_t v = vals[e];
   const int32_t a = (int32_t)(v >> 5), c = (int32_t)(v & 31u);
   const int32_t u = act[a];
-  inv[(int64_t)a * K + c] = e;
+  inv[(int64_t)a * K + c] = e;  // sort mode: no row is long (the round's minima only)
   // operands of entry e, laid out in bidder order so that a window's loads in
   // k_accept are independent and coalesced (no unit -> request gather chain)
   ent_unit[e] = u;
@@ -232,43 +239,55 @@ __global__ void k_csr_finish(int32_t P, int32_t N, int32_t K, int32_t D, int32_t
 
 // ---- node -> bidder index by counting (no sort) ----------------------------------
 // k_csr_keys sets bit a of row n of a [N][Wb] bitmap (Wb = ceil(A/32)) for
-// every candidate n of slot a. k_csr_rows (one wave per row) turns it into,
-// per nonzero word, {rank of the word's first set bit within the row, the
-// bits} and the row length, and clears the row; k_csr_scan (one workgroup)
-// scans the row lengths into node segments (node order). k_csr_place then
-// gives candidate (a, c) its entry e = segment start + rank of bit a, so each
-// node's bidder row is in slot (= rank) order: a stable counting sort keyed by
-// node id. (Measured alternatives to the separate scan launch, ~12 us per
-// round for rows + scan: a last-workgroup-done scan inside k_csr_rows needs a
-// device-scope fence per wave, 150-280 us per launch; a decoupled look-back
-// over the 16-row blocks, 16 us per launch.)
-__global__ __launch_bounds__(64 * KP_ROWS_WPB) void k_csr_rows(int32_t N, int64_t Wb,
+// every candidate n of slot a, and the first bit of a word sets the word's bit
+// in the row's summary ([N][Ws], Ws = ceil(Wb/32)). k_csr_rows (one wave per
+// row) walks the summary, 64 summary words (2,048 bitmap words) per step, and
+// turns every nonzero bitmap word into {rank of its first set bit within the
+// row, the bits}, counts the row and clears what it read: a herded round
+// (config #4: 200k slots x 16 candidates over ~1,300 of 20k nodes, 125M
+// bitmap words) reads the 4M summary words and its 3M nonzero words, not the
+// whole bitmap. k_csr_scan (one workgroup) scans the row lengths into node
+// segments (node order). k_csr_place then gives candidate (a, c) its entry e
+// = segment start + rank of bit a, so each node's bidder row is in slot
+// (= rank) order: a stable counting sort keyed by node id. (Measured
+// alternatives to the separate scan launch, ~12 us per round for rows + scan:
+// a last-workgroup-done scan inside k_csr_rows needs a device-scope fence per
+// wave, 150-280 us per launch; a decoupled look-back over the 16-row blocks,
+// 16 us per launch.)
+__global__ __launch_bounds__(64 * KP_ROWS_WPB) void k_csr_rows(int32_t N, int64_t Wb, int64_t Ws,
                                                    uint32_t *__restrict__ bm,
+                                                   uint32_t *__restrict__ bms,
                                                    uint2 *__restrict__ rowinfo,
                                                    int32_t *__restrict__ cnt) {
   const int lane = threadIdx.x & 63;
   const int n = blockIdx.x * KP_ROWS_WPB + (threadIdx.x >> 6);
   if (n >= N) return;  // wave-uniform
-  const int64_t rb = (int64_t)n * Wb;
+  const int64_t rb = (int64_t)n * Wb, sb = (int64_t)n * Ws;
   int32_t tot = 0;
-  for (int64_t w0 = 0; w0 < Wb; w0 += 256) {
-    uint32_t b[4];
+  for (int64_t s0 = 0; s0 < Ws; s0 += 64) {
+    const int64_t sw_i = s0 + lane;
+    const uint32_t sw = sw_i < Ws ? bms[sb + sw_i] : 0u;
+    if (__ballot(sw != 0u) == 0) continue;
+    // the (up to 32) nonzero bitmap words of this lane's summary word, loaded
+    // together (a set summary bit implies the word is inside the row)
+    const int64_t wb = rb + sw_i * 32;
+    uint32_t b[32];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {  // four independent loads in flight
-      const int64_t w = w0 + i * 64 + lane;
-      b[i] = w < Wb ? bm[rb + w] : 0u;
-    }
+    for (int i = 0; i < 32; ++i) b[i] = (sw >> i) & 1u ? bm[wb + i] : 0u;
+    int32_t c = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int32_t c = __popc(b[i]);
-      const int32_t inc = wave_incl_scan_i32(c);
+    for (int i = 0; i < 32; ++i) c += __popc(b[i]);
+    const int32_t inc = wave_incl_scan_i32(c);
+    int32_t pre = tot + inc - c;
+#pragma unroll
+    for (int i = 0; i < 32; ++i)
       if (b[i]) {
-        const int64_t w = w0 + i * 64 + lane;
-        rowinfo[rb + w] = make_uint2((uint32_t)(tot + inc - c), b[i]);
-        bm[rb + w] = 0u;  // the bitmap is all-zero between rounds
+        rowinfo[wb + i] = make_uint2((uint32_t)pre, b[i]);
+        bm[wb + i] = 0u;  // the bitmap is all-zero between rounds
+        pre += __popc(b[i]);
       }
-      tot += __builtin_amdgcn_readlane(inc, 63);
-    }
+    if (sw) bms[sb + sw_i] = 0u;
+    tot += __builtin_amdgcn_readlane(inc, 63);
   }
   if (lane == 0) cnt[n] = tot;
 }
@@ -363,6 +382,7 @@ __global__ void k_csr_place(int32_t A, int32_t K, int32_t D, int32_t U, int64_t 
                             const int32_t *__restrict__ act, const int64_t *__restrict__ q,
                             const int32_t *__restrict__ size, const int32_t *__restrict__ leader,
                             const int32_t *__restrict__ seg_start,
+                            const int32_t *__restrict__ cnt, int32_t bmin_windows,
                             const uint2 *__restrict__ rowinfo, int32_t *__restrict__ inv,
                             int32_t *__restrict__ ent_unit, int32_t *__restrict__ ent_slot,
                             int32_t *__restrict__ ent_size, int32_t *__restrict__ ent_lead,
@@ -374,10 +394,13 @@ __global__ void k_csr_place(int32_t A, int32_t K, int32_t D, int32_t U, int64_t 
   const int32_t a = (int32_t)(t / K);
   const int32_t u = act[a];
   if (n < 0) return;
-  const int32_t ss = seg_start[n];
+  const int32_t ss = seg_start[n], len = cnt[n];
   const uint2 ri = rowinfo[(int64_t)n * Wb + (a >> 5)];
   const int32_t e = ss + (int32_t)ri.x + __popc(ri.y & ((1u << (a & 31)) - 1u));
-  inv[t] = e;
+  // bit 31: the entry's bidder row spans >= bmin_windows windows (the plan
+  // keeps exact per-pass window minima for those rows only)
+  const bool lrow = ((ss + len - 1) >> 6) - (ss >> 6) + 1 >= bmin_windows;
+  inv[t] = e | (lrow ? (int32_t)0x80000000u : 0);
   // operands of entry e in bidder order (k_accept's window loads)
   ent_unit[e] = u;
   ent_slot[e] = a;
@@ -421,6 +444,7 @@ struct PlanArgs {
   const int32_t *ptot;
   const int64_t *ent_q;
   int64_t *winmin;
+  int64_t *bmin;  // long rows: per-window bid minima of the pass
   uint32_t key_off;        // W32 member loop: 64 * w_spread + 1 (plan_key_ok)
   uint64_t *pp;            // KP_PASS_PROFILE only
   const SolveStats *st;    // KP_PASS_PROFILE only (round index)
@@ -446,7 +470,9 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
   const uint8_t op = pa.open[aa];
   const int32_t u0 = pa.act[aa];
   const int32_t node = gl < K ? pa.cand[(int64_t)aa * K + gl] : -1;
-  const int32_t e_inv = gl < K ? pa.inv[(int64_t)aa * K + gl] : 0;  // valid iff node >= 0
+  // valid iff node >= 0; bit 31: the entry's bidder row is long (k_csr_place)
+  const int32_t inv_raw = gl < K ? pa.inv[(int64_t)aa * K + gl] : 0;
+  const int32_t e_inv = inv_raw & 0x7FFFFFFF;
   const int32_t prev = pass > 0 ? pa.pass_flag[pass - 1] : 1;
   const int32_t A = pa.A_dev ? min(pa.A, *pa.A_dev) : pa.A;
   // a pass after one without proposals has none either (usage unchanged,
@@ -565,7 +591,6 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
           for (int d = 0; d < D; ++d) {
             rem[d] -= q32[d];
             const bool wrap = r_[d] >= thr[d];
-            t_[d] += Q_[d] + (wrap ? 1u : 0u);
             r_[d] = wrap ? r_[d] - thr[d] : r_[d] + rho[d];
             acc_t += wq[d] + (wrap ? sp.w[d] : 0);
           }
@@ -621,7 +646,26 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
     // bid tag: pass << 16 | parts << 8 | members (parts <= K <= 32, members <= 64)
     pa.bid[e_inv] = ((uint32_t)pass << 16) | ((uint32_t)np << 8) | (uint32_t)planned;
     pa.s0_out[e_inv] = s0;
-    pa.win[e_inv >> 6] = pass;
+    // Long rows (k_csr_place, >= KP_BMIN_WIN windows): the window's smallest
+    // bid of this pass per dim — tighter than the round's smallest request,
+    // so accept skips, unread, the windows of a herded row none of whose
+    // bids of this pass fits (config #4's tail); the pass tag in the high
+    // bits makes atomicMax keep this pass's minimum. Short rows only flag
+    // the window (one plain store: atomics for every bid cost a config #3
+    // solve ~2.3 ms), which also tells accept the bid minima do not bound
+    // every bid of the window.
+    if (inv_raw < 0) {
+      const uint64_t tag = (uint64_t)(pass + 1) << 48, lo = (1ull << 48) - 1;
+      int64_t *bw = pa.bmin + (e_inv >> 6);
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const uint64_t need = (uint64_t)planned * (uint64_t)qq[d];
+        atomicMax(reinterpret_cast<unsigned long long *>(bw + (int64_t)d * pa.nwin),
+                  (unsigned long long)(tag | (lo - (need < lo ? need : lo))));
+      }
+    } else {
+      pa.win[e_inv >> 6] = pass;
+    }
     pa.node_flag[node] = pass;
     if (np > 1) {
       const int idx = __popcll(pm & ((1ull << gl) - 1));
@@ -869,8 +913,10 @@ struct AccArgs {
   const int64_t *cap;
   const int32_t *node_flag, *node_list, *nl_count, *pass_flag;
   const int4 *nrec;
-  const int64_t *winmin;
+  const int64_t *winmin;  // the round's smallest request per window
+  const int64_t *bmin;    // long rows: this pass's smallest bid per window, tagged (k_plan)
   int64_t nwin;
+  int32_t bmin_windows;   // rows spanning at least this many windows are long
   AcceptOut o;
   // host-followed passes: this pass's flag, tagged with the round serial, to
   // coherent host memory (the host enqueues further passes only while it is set)
@@ -922,16 +968,33 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
     for (int wb = w0; wb <= w1; wb += 64) {
       const int wi = wb + lane;
       const bool mine = wi <= w1;
+      // window wi: the round's smallest request per dim, a short row's bid
+      // of this pass, and on a long row this pass's smallest long-row bid
+      // per dim (tag pass + 1; older tags: none)
+      const bool lrow = w1 - w0 + 1 >= ac.bmin_windows;  // wave-uniform, as k_csr_place
       int64_t wmin[D];
+      uint64_t braw[D];
 #pragma unroll
-      for (int d = 0; d < D; ++d) wmin[d] = mine ? ac.winmin[(int64_t)d * ac.nwin + wi] : 0;
+      for (int d = 0; d < D; ++d) {
+        wmin[d] = mine ? ac.winmin[(int64_t)d * ac.nwin + wi] : 0;
+        braw[d] = mine && lrow ? (uint64_t)ac.bmin[(int64_t)d * ac.nwin + wi] : 0;
+      }
       const int32_t wf = mine ? ac.win[wi] : -1;
       if (wb == w0) {  // the first chunk's flags were loaded with the node's operands
         KP_PP_MARK(0);
         if (nf != pass) return;
         KP_PP_WORK();
       }
-      uint64_t flagged = __ballot(wf == pass);
+      uint64_t flagged = __ballot(wf == pass || (braw[0] >> 48) == (uint64_t)(pass + 1));
+      // the bid minima bound every bid of the window unless a short row bid
+      // in it too (a dim without this pass's tag: no long-row bid)
+      if (lrow) {
+        constexpr uint64_t kLo = (1ull << 48) - 1;
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+          if (wf != pass && (braw[d] >> 48) == (uint64_t)(pass + 1))
+            wmin[d] = max(wmin[d], (int64_t)(kLo - (braw[d] & kLo)));
+      }
       KP_PP_MARK(1);
       while (true) {
         bool can = true;
@@ -1051,6 +1114,7 @@ static PlanArgs plan_args(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t p
   pa.ptot = c->d.counters + 33;
   pa.ent_q = c->d.ent_q;
   pa.winmin = c->d.winmin;
+  pa.bmin = c->d.bmin;
   pa.node_list = c->d.node_list;
   pa.nl_count = c->d.counters + 32;
   pa.seg_start = c->d.seg_start;
@@ -1083,6 +1147,8 @@ static AccArgs acc_args(kp_ctx *c, const ScoreParams &sp, int64_t P) {
   ac.nl_count = c->d.counters + 32;
   ac.pass_flag = c->d.pass_flag;
   ac.winmin = c->d.winmin;
+  ac.bmin = c->d.bmin;
+  ac.bmin_windows = c->bmin_windows;
   ac.nwin = (P + 63) / 64 + 64;
   AcceptOut &o = ac.o;
   o.N = c->N;
@@ -1194,14 +1260,16 @@ static int ensure_bitmap(kp_ctx *c, int64_t words) {
   if (grow) {
     c->cap_bm_words = 0;
     c->cap_cnt_N = 0;
-    for (void **p : {(void **)&c->d.bm, (void **)&c->d.rowinfo, (void **)&c->d.cnt})
+    for (void **p : {(void **)&c->d.bm, (void **)&c->d.bms, (void **)&c->d.rowinfo, (void **)&c->d.cnt})
       if (*p) {
         (void)hipFree(*p);
         *p = nullptr;
       }
     const int64_t w = std::max<int64_t>(words, 64);
     const int32_t nc = std::max(c->N, 64);
+    // the summary: N x ceil(Wb/32) <= words/32 + N words
     if (hipMalloc(reinterpret_cast<void **>(&c->d.bm), sizeof(uint32_t) * w) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&c->d.bms), sizeof(uint32_t) * (w / 32 + nc + 64)) != hipSuccess ||
         hipMalloc(reinterpret_cast<void **>(&c->d.rowinfo), sizeof(uint2) * w) != hipSuccess ||
         hipMalloc(reinterpret_cast<void **>(&c->d.cnt), sizeof(int32_t) * nc) != hipSuccess)
       return KP_ENOMEM;
@@ -1210,8 +1278,11 @@ static int ensure_bitmap(kp_ctx *c, int64_t words) {
   }
   // all-zero between rounds (k_csr_rows clears what k_csr_keys set); a
   // round cut short between the two is repaired here
-  if (grow || c->bm_dirty)
+  if (grow || c->bm_dirty) {
     KP_HIP(hipMemsetAsync(c->d.bm, 0, sizeof(uint32_t) * c->cap_bm_words, c->stream));
+    KP_HIP(hipMemsetAsync(c->d.bms, 0, sizeof(uint32_t) * (c->cap_bm_words / 32 + c->cap_cnt_N + 64),
+                          c->stream));
+  }
   c->bm_dirty = false;
   return KP_OK;
 }
@@ -1253,8 +1324,12 @@ RoundKeys round_keys_args(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev)
   rk.Wb = ((int64_t)A + 31) / 32;
   rk.init_n = std::max<int64_t>(std::max<int64_t>(c->N, rk.nwin), 64);
   rk.bm = c->d.bm;
+  rk.bms = c->d.bms;
+  rk.Ws = (rk.Wb + 31) / 32;
   rk.bid = c->d.bid;
+  rk.bmin = c->d.bmin;
   rk.win = c->d.win;
+  rk.D = c->D;
   rk.seg_start = c->d.seg_start;
   rk.pass_flag = c->d.pass_flag;
   rk.node_flag = c->d.node_flag;
@@ -1276,17 +1351,19 @@ int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev) {
   } else {
     KP_TRY(csr_prepare(c, A, K));
     uint32_t *bm = c->csr_mode ? c->d.bm : nullptr;
+    const int64_t Ws = (Wb + 31) / 32;
     hipLaunchKernelGGL(k_csr_keys, dim3(blocks(n, 256)), dim3(256), 0, c->stream, A, K, c->N, nwin,
-                       c->d.cand, c->d.csr_kin, c->d.csr_vin, c->d.bid, c->d.win, c->d.seg_start,
+                       c->d.cand, c->d.csr_kin, c->d.csr_vin, c->d.bid, c->d.win, c->d.bmin, c->D,
+                       c->d.seg_start,
                        c->d.pass_flag, c->d.node_flag, c->d.counters + 32, A_dev, c->d.stats,
-                       c->d.act, c->d.open, c->d.status, bm, Wb);
+                       c->d.act, c->d.open, c->d.status, bm, c->d.bms, Wb, Ws);
     KP_HIP(hipGetLastError());
   }
   if (P == 0) return KP_OK;
   if (c->csr_mode) {
     hipLaunchKernelGGL(k_csr_rows, dim3((unsigned)((c->N + KP_ROWS_WPB - 1) / KP_ROWS_WPB)),
                        dim3(64 * KP_ROWS_WPB), 0, c->stream,
-                       c->N, Wb, c->d.bm, c->d.rowinfo, c->d.cnt);
+                       c->N, Wb, (Wb + 31) / 32, c->d.bm, c->d.bms, c->d.rowinfo, c->d.cnt);
     KP_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_csr_scan, dim3(1), dim3(1024), 0, c->stream, c->N, c->d.cnt,
                        c->d.seg_start, c->d.seg_end, c->d.node_list, c->d.nrec,
@@ -1295,7 +1372,8 @@ int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev) {
     c->bm_dirty = false;
     hipLaunchKernelGGL(k_csr_place, dim3(blocks(P, 256)), dim3(256), 0, c->stream, A, K, c->D,
                        c->U, Wb, P, A_dev, c->d.cand, c->d.act, c->d.q, c->d.size, c->d.leader,
-                       c->d.seg_start, c->d.rowinfo, c->d.inv, c->d.ent_unit, c->d.ent_slot,
+                       c->d.seg_start, c->d.cnt, c->bmin_windows, c->d.rowinfo, c->d.inv,
+                       c->d.ent_unit, c->d.ent_slot,
                        c->d.ent_size, c->d.ent_lead, c->d.ent_q);
     KP_HIP(hipGetLastError());
     return KP_OK;

@@ -168,7 +168,8 @@ __device__ __forceinline__ void pack_node(const int64_t *__restrict__ cap,
                                           const int32_t *__restrict__ perm,
                                           const int32_t *__restrict__ colnode, int32_t N,
                                           int32_t P, bool full, const ScoreParams &sp,
-                                          uint32_t *__restrict__ np, int i) {
+                                          uint32_t *__restrict__ np, int i,
+                                          const uint32_t *__restrict__ ncls) {
   // colnode: column -> node, -1 = padding; the free plane of dim 0 then holds
   // free + 1 (0 on padding), so that the fused kernel's fit test also rejects
   // padding columns
@@ -209,6 +210,8 @@ __device__ __forceinline__ void pack_node(const int64_t *__restrict__ cap,
   if (full) {
     np[(int64_t)(kPlanes * D) * P + i] = v ? (uint32_t)base[n] : 0u;
     np[(int64_t)(kPlanes * D + 1) * P + i] = v ? (uint32_t)topo[n] : 0xFFFFFFFFu;
+    // capacity class (k_score32's class form; padding: class 0, masked by N)
+    np[(int64_t)(kPlanes * D + 3) * P + i] = v && ncls ? ncls[n] : 0u;
   }
   np[(int64_t)(kPlanes * D + 2) * P + i] = wa;
 }
@@ -229,11 +232,12 @@ __global__ __launch_bounds__(256) void k_round_start(const int32_t *__restrict__
                                                      const int32_t *__restrict__ perm,
                                                      const int32_t *__restrict__ colnode, int32_t N,
                                                      int32_t P, int32_t full, ScoreParams sp,
-                                                     uint32_t *__restrict__ np) {
+                                                     uint32_t *__restrict__ np,
+                                                     const uint32_t *__restrict__ ncls) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < hi - lo) flag[i] = status[lo + i] == kActive ? 1 : 0;
   if (i < P)
-    pack_node<D>(cap, used, R32, K32, base, topo, perm, colnode, N, P, full != 0, sp, np, i);
+    pack_node<D>(cap, used, R32, K32, base, topo, perm, colnode, N, P, full != 0, sp, np, i, ncls);
 }
 
 // bit j of a 32-bit value -> bit 2j
@@ -577,6 +581,148 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
   score_rows_mixed<D, MOST, NPL>(sp, sq, r0, r1, pv, PV, iv, f_, fg_, tp_, b_, v_, score, mask, Ns,
                                  tile0, nb, lane);
 #endif
+}
+
+// Class form of k_score32: node tables with at most kScoreClasses distinct
+// capacity vectors (a cluster of a few node shapes: every BASELINE config).
+// The workgroup stages, per (row, class), the thresholds c - rho and WQ
+// (q*S = Q*c + rho: one exact division per row, class and dim) and every pair
+// takes score_rows_uniform's compare-and-select form with its node's class
+// (the class plane of the pack, kPlanes*D + 3) — no per-pair division on any
+// wave. kp_score returns node order, where the classes interleave, so the
+// uniform-wave test of k_score32 fails on almost every wave there.
+// Columns are STRIDED over the lanes: a wave owns 256 columns, lane l the
+// columns base + 64k + l (k < 4), so each ballot of the fit flags IS a mask
+// word (no bit interleaving per row: that per-row chain cost as much as the
+// score stores, tools/score_dev_time.py) and every store instruction writes
+// 256 contiguous bytes. A workgroup's 1,024 columns are 16 mask words, one
+// 128-B line when the row stride is a multiple of 16 words (kp_score_dev).
+// Rows are written with the given strides (the internal chunk, or the
+// caller's device buffers of kp_score_dev).
+constexpr int kScoreClsRows = 64;  // rows per workgroup (LDS: rows x classes x record)
+constexpr int kClsCols = 4;        // columns per lane
+
+template <int D, bool MOST>
+__global__ __launch_bounds__(256) void k_score32c(
+    ScoreParams sp, const uint32_t *__restrict__ np, int32_t P, const int64_t *__restrict__ q,
+    int32_t qstride, const int32_t *__restrict__ uaff, const int32_t *__restrict__ rows_unit,
+    int32_t rows, int32_t rows_per_block, int32_t min_rpb, int32_t *__restrict__ score,
+    int64_t sstride, uint64_t *__restrict__ mask, int64_t mstride, int32_t Ns,
+    const int32_t *__restrict__ rows_dev, const uint32_t *__restrict__ ccap, int32_t ncl) {
+  constexpr int NC = kClsCols;
+  constexpr int RW = (D + 1 + 3) & ~3;  // per (row, class): D thresholds + WQ, whole 16-B reads
+  if (rows_dev) fit_rows(*rows_dev, min_rpb, rows, rows_per_block);
+  if ((int)blockIdx.y * rows_per_block >= rows) return;  // block-uniform
+  __shared__ uint32_t sq[kScoreClsRows][D + 2];
+  __shared__ __attribute__((aligned(16))) uint32_t sx[kScoreClsRows][kScoreClasses][RW];
+  const int N = sp.N;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tile0 = blockIdx.x * (256 * NC) + wave * (64 * NC);  // this wave's first column
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  const int nr = r1 - r0;
+  const int g = sp.gpu_dim;
+  for (int i = threadIdx.x; i < nr * (D + 2); i += blockDim.x) {
+    const int rr = i / (D + 2), d = i % (D + 2);
+    const int32_t unit = rows_unit[r0 + rr];
+    uint32_t v;
+    if (d == D + 1) {
+      v = (uint32_t)uaff[unit];
+    } else {
+      const int dd = d < D ? d : g;
+      v = dd >= 0 ? (uint32_t)q[(int64_t)dd * qstride + unit] : 0u;
+    }
+    sq[rr][d] = v;
+  }
+  // the lane's columns tile0 + 64k + lane (P % 1024 == 0: inside the planes)
+  uint32_t f_[NC][D], a_[NC][D], fg_[NC], tp_[NC], cl_[NC];
+  int32_t b_[NC], wa_[NC];
+  bool v_[NC];
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    const int64_t col = tile0 + 64 * k + lane;
+    v_[k] = col < N;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      f_[k][d] = np[(int64_t)(kPlanes * d + 0) * P + col];
+      a_[k][d] = np[(int64_t)(kPlanes * d + 2) * P + col];
+    }
+    b_[k] = (int32_t)np[(int64_t)(kPlanes * D) * P + col];
+    tp_[k] = np[(int64_t)(kPlanes * D + 1) * P + col];
+    wa_[k] = (int32_t)np[(int64_t)(kPlanes * D + 2) * P + col];
+    cl_[k] = min(np[(int64_t)(kPlanes * D + 3) * P + col], (uint32_t)(kScoreClasses - 1));
+    fg_[k] = 0xFFFFFFFFu;  // free GPUs: never equal to a request when there is no GPU dim
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      if (d == g) fg_[k] = f_[k][d];
+  }
+  __syncthreads();  // requests staged
+  {
+    // per (row, class): q*S = Q*c + rho in every dim, one thread each
+    const uint64_t S = (uint64_t)sp.S;
+    for (int t = threadIdx.x; t < ncl * nr; t += blockDim.x) {
+      const int k = t / nr, rr = t - k * nr;
+      uint32_t wq = 0;
+      bool ok = true;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const uint32_t c = ccap[k * D + d], qd = sq[rr][d];
+        uint32_t thr = 0xFFFFFFFFu;  // cap-0 dim: contributes 0, fits only q = 0
+        if (c == 0u) {
+          ok &= qd == 0u;
+        } else if (qd > c) {
+          ok = false;
+        } else {
+          uint64_t Q, rho;
+          udivmod_uniform((uint64_t)qd * S, c, Q, rho);
+          thr = c - (uint32_t)rho;  // in (0, c]: carry iff a >= thr
+          wq += (uint32_t)sp.w[d] * (uint32_t)Q;
+        }
+        sx[rr][k][d] = thr;
+      }
+      sx[rr][k][D] = ok ? wq : kRowNoFit;
+    }
+  }
+  __syncthreads();
+  if (tile0 >= Ns) return;  // wave-uniform, after the last barrier
+  const int32_t wfit = sp.w_gpu_fit, waff = sp.w_affinity;
+  for (int r = r0; r < r1; ++r) {
+    uint32_t qq[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) qq[d] = sq[r - r0][d];
+    const uint32_t qg = sq[r - r0][D], af = sq[r - r0][D + 1];
+    int32_t *srow = score ? score + (int64_t)r * sstride + tile0 + lane : nullptr;
+    uint64_t word[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      uint32_t x[RW];
+#pragma unroll
+      for (int i = 0; i < RW / 4; ++i) {
+        const uint4 t4 = reinterpret_cast<const uint4 *>(sx[r - r0][cl_[k]])[i];
+        x[4 * i] = t4.x;
+        x[4 * i + 1] = t4.y;
+        x[4 * i + 2] = t4.z;
+        x[4 * i + 3] = t4.w;
+      }
+      bool ft = v_[k] && !(x[D] & kRowNoFit);
+      int32_t acc = wa_[k] + (int32_t)(x[D] & ~kRowNoFit);
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        ft &= qq[d] <= f_[k][d];
+        acc += a_[k][d] >= x[d] ? sp.w[d] : 0;
+      }
+      const int32_t bonus = ((qg != 0u && fg_[k] == qg) ? wfit : 0) + (tp_[k] == af ? waff : 0);
+      const int32_t sc = (MOST ? acc : b_[k] - acc) + bonus;
+      if (srow && tile0 + 64 * k < Ns) srow[64 * k] = ft ? sc : KP_SCORE_INFEASIBLE;
+      word[k] = __ballot(ft);  // columns tile0 + 64k .. + 63: mask word (tile0 >> 6) + k
+    }
+    if (mask && lane < NC && tile0 + 64 * lane < Ns) {
+      uint64_t wd = word[0];
+#pragma unroll
+      for (int k = 1; k < NC; ++k) wd = lane == k ? word[k] : wd;
+      mask[(int64_t)r * mstride + (tile0 >> 6) + lane] = wd;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1030,13 +1176,13 @@ __global__ __launch_bounds__(kCompactBS) void k_round_begin(
     const uint32_t *__restrict__ R32, const uint32_t *__restrict__ K32,
     const int64_t *__restrict__ base, const int32_t *__restrict__ topo,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ colnode, int32_t N, int32_t P,
-    int32_t full, ScoreParams sp, uint32_t *__restrict__ np) {
+    int32_t full, ScoreParams sp, uint32_t *__restrict__ np, const uint32_t *__restrict__ ncls) {
   if (blockIdx.x == 0) {
     compact_wg<true>(status, n, lo, out, count, host_count);
     return;
   }
   const int i = (blockIdx.x - 1) * kCompactBS + threadIdx.x;
-  if (i < P) pack_node<D>(cap, used, R32, K32, base, topo, perm, colnode, N, P, full != 0, sp, np, i);
+  if (i < P) pack_node<D>(cap, used, R32, K32, base, topo, perm, colnode, N, P, full != 0, sp, np, i, ncls);
 }
 
 template <int D>
@@ -1048,7 +1194,7 @@ struct RoundBeginL {
                        c->d.cap, c->d.used, c->d.R32, c->d.K32, c->d.base, c->d.topo,
                        c->pack_canonical ? c->d.perm : nullptr,
                        c->pack_fused ? c->d.colnode : nullptr, c->N, P, c->pack_full ? 1 : 0,
-                       c->pack_sp, c->d.np32);
+                       c->pack_sp, c->d.np32, c->n_classes > 0 ? c->d.ncls : nullptr);
     KP_HIP(hipGetLastError());
     if (P > 0) c->pack_full = false;  // capacity planes in place for this layout
     return KP_OK;
@@ -1059,7 +1205,7 @@ template <int D>
 struct ScoreL {
   static int run(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
                  int32_t *score, uint64_t *mask, const int64_t *q, int32_t qstride,
-                 const int32_t *rows_dev) {
+                 const int32_t *rows_dev, int64_t sstride, int64_t mstride) {
     const int Ns = (c->N + 63) & ~63;
     if (c->fits32) {
       const int P = (c->N + 1023) & ~1023;  // planes from the round start (launch_pack)
@@ -1069,6 +1215,25 @@ struct ScoreL {
       // resident waves) unless KP_SCORE_NPL=4
       const int npl = c->score_npl;
       const int tiles = blocks(Ns, 256 * npl);
+      if (c->n_classes > 0 && c->score_classes) {  // the class form (every wave, either order)
+        const int ctiles = blocks(Ns, 256 * kClsCols);
+        const int64_t want = ((int64_t)rows * ctiles + c->score_wg_target - 1) / c->score_wg_target;
+        const int rpb =
+            (int)std::min<int64_t>(kScoreClsRows, std::max<int64_t>(c->score_min_rpb, want));
+        const dim3 grid(ctiles, blocks(rows, rpb));
+#define KP_SC32C(M)                                                                           \
+  hipLaunchKernelGGL((k_score32c<D, M>), grid, dim3(256), 0, c->stream, sp, c->d.np32, P, q,      \
+                     qstride, c->d.aff, rows_unit, rows, rpb, c->score_min_rpb, score,            \
+                     sstride > 0 ? sstride : (int64_t)Ns, mask, mstride > 0 ? mstride : (int64_t)Ns / 64, \
+                     Ns, rows_dev, c->d.ccap, c->n_classes)
+        if (sp.most_allocated)
+          KP_SC32C(true);
+        else
+          KP_SC32C(false);
+#undef KP_SC32C
+        KP_HIP(hipGetLastError());
+        return KP_OK;
+      }
       const int64_t want = ((int64_t)rows * tiles + c->score_wg_target - 1) / c->score_wg_target;
       const int rpb =
           (int)std::min<int64_t>(kScoreMaxRows, std::max<int64_t>(c->score_min_rpb, want));
@@ -1114,9 +1279,10 @@ int launch_prep_nodes(kp_ctx *c, int32_t S, int most_allocated, const int32_t *w
 
 int launch_score(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
                  int32_t *score, uint64_t *mask, const int64_t *q, int32_t qstride,
-                 const int32_t *rows_dev) {
+                 const int32_t *rows_dev, int64_t sstride, int64_t mstride) {
   if (rows <= 0 || c->N == 0) return KP_OK;
-  return dispatch_D<ScoreL>(c->D, c, sp, rows_unit, rows, score, mask, q, qstride, rows_dev);
+  return dispatch_D<ScoreL>(c->D, c, sp, rows_unit, rows, score, mask, q, qstride, rows_dev,
+                            sstride, mstride);
 }
 
 // Threshold-select shapes (V4 16-B loads per thread x BS threads cover
@@ -1206,7 +1372,7 @@ struct RoundStartL {
                        c->d.status, lo, hi, flag, c->d.cap, c->d.used, c->d.R32, c->d.K32,
                        c->d.base, c->d.topo, c->pack_canonical ? c->d.perm : nullptr,
                        c->pack_fused ? c->d.colnode : nullptr, c->N, P, c->pack_full ? 1 : 0,
-                       c->pack_sp, c->d.np32);
+                       c->pack_sp, c->d.np32, c->n_classes > 0 ? c->d.ncls : nullptr);
     KP_HIP(hipGetLastError());
     if (P > 0) c->pack_full = false;  // capacity planes in place for this layout
     return KP_OK;

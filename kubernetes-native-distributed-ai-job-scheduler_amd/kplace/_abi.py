@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-KP_ABI_VERSION = 5
+KP_ABI_VERSION = 6
 KP_MAX_DIMS = 8
 KP_MAX_CAND = 32
 KP_MAX_GANG = 64
@@ -94,8 +94,8 @@ class Timing(C.Structure):
         ("solve_ms", C.c_double), ("score_ms", C.c_double),
         ("select_ms", C.c_double), ("accept_ms", C.c_double),
         ("score_launches", C.c_int64), ("score_bytes", C.c_int64),
-        ("select_bytes", C.c_int64), ("fused", C.c_int32), ("loop_rounds", C.c_int32),
-        ("incr_rounds", C.c_int32), ("pad", C.c_int32),
+        ("select_bytes", C.c_int64), ("fused", C.c_int32), ("score_form", C.c_int32),
+        ("score_classes", C.c_int32), ("pad", C.c_int32),
     ]
 
 
@@ -141,7 +141,8 @@ def params_dict(p: Params) -> dict:
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 # KPLACE_LIB: an alternative build of the same library (A/B timing runs only)
-LIB_PATH = os.environ.get("KPLACE_LIB") or os.path.join(os.path.dirname(PKG_DIR), "libkplace.so")
+_DEFAULT_LIB = os.path.join(os.path.dirname(PKG_DIR), "libkplace.so")
+LIB_PATH = os.environ.get("KPLACE_LIB") or _DEFAULT_LIB
 
 
 # kp_allgather_fn: (user, send, bytes, recv) -> 0 on success
@@ -174,6 +175,7 @@ def load_library(path: str | None = None) -> C.CDLL:
         "kp_apply_delta": (C.c_int, [vp, _i32p, _i64p, C.c_int32]),
         "kp_reset_nodes": (C.c_int, [vp]),
         "kp_score": (C.c_int, [vp, C.POINTER(Params), C.c_int32, C.c_int32, _i32p, _u64p]),
+        "kp_score_dev": (C.c_int, [vp, C.POINTER(Params), C.c_int32, C.c_int32, vp, vp]),
         "kp_last_timing": (C.c_int, [vp, C.POINTER(Timing)]),
         "kp_set_profiling": (C.c_int, [vp, C.c_int]),
         "kp_set_allgather": (C.c_int, [vp, ALLGATHER_FN, vp]),
@@ -182,6 +184,8 @@ def load_library(path: str | None = None) -> C.CDLL:
         "kp_preempt": (C.c_int, [vp, C.POINTER(Preemption)]),
     }
     for name, (res, args) in sigs.items():
+        if (path or LIB_PATH) != _DEFAULT_LIB and not hasattr(lib, name):
+            continue  # an explicitly named older build (A/B runs): entry points it lacks stay absent
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -195,5 +199,5 @@ EXPORTED = (
     "kp_abi_version", "kp_dist_unique_id", "kp_place", "kp_load_nodes",
     "kp_load_jobs", "kp_solve", "kp_fetch", "kp_apply_delta", "kp_reset_nodes", "kp_score",
     "kp_last_timing", "kp_set_profiling", "kp_parse_gpu_memory", "kp_load_running",
-    "kp_preempt", "kp_set_allgather",
+    "kp_preempt", "kp_set_allgather", "kp_score_dev",
 )

@@ -207,6 +207,14 @@ class Placer:
                               _ptr(mk, C.c_uint64)), "kp_score", self._h)
         return sc, mk
 
+    def score_dev(self, params: _abi.Params, lo: int, hi: int, score_ptr: int | None,
+                  mask_ptr: int | None) -> None:
+        """kp_score_dev: the filter + score pass into caller-owned device memory
+        (raw device addresses, e.g. torch.Tensor.data_ptr(); rows of
+        Ns = round_up(N, 64) int32 scores and Ns / 64 uint64 mask words)."""
+        _check(lib().kp_score_dev(self._h, C.byref(params), lo, hi, C.c_void_p(score_ptr or None),
+                                  C.c_void_p(mask_ptr or None)), "kp_score_dev", self._h)
+
     def set_profiling(self, on: bool) -> None:
         _check(lib().kp_set_profiling(self._h, 1 if on else 0), "kp_set_profiling", self._h)
 

@@ -314,6 +314,33 @@ def test_accept_long_row_form_parity(oracle, monkeypatch, seed):
     _assert_same(g2, o, f"accept long-row form seed {seed}, second solve")
 
 
+@pytest.mark.parametrize("win", ["1", "2", "8"])
+@pytest.mark.parametrize("case", ["config4", "gangs", "big_caps"])
+def test_long_row_bid_minima_parity(oracle, monkeypatch, win, case):
+    """Per-pass window bid minima of long bidder rows (plan atomicMax, tagged
+    with the pass) forced on rows of >= KP_BMIN_WIN windows — with 1 every
+    row, so windows that straddle a long and a short row, gang bids (members
+    x request) and 64-bit requests all meet accept's skip test. Same
+    placement as the oracle, a second solve too (stale tags of the previous
+    round or solve never skip a window)."""
+    monkeypatch.setenv("KP_BMIN_WIN", win)
+    if case == "config4":
+        w = synth.config4(20_000, 2_000)
+        p = _abi.default_params(**synth.CONFIG_PARAMS[4])
+    else:
+        w = random_workload(700 + int(win), J=4000, N=300, max_gang=8)
+        if case == "big_caps":
+            w = synth.Workload(w.J, w.N, w.D, w.req * (1 << 22), w.cap * (1 << 22), w.used * (1 << 22),
+                               w.prio, w.gang_id, w.gang_size, w.topo, name="rand_big_caps")
+        p = _abi.default_params(score_mode=int(win) % 2, n_cand=16)
+    with Placer(device=0) as pl:
+        g = pl.place(w, p)
+        g2 = pl.place(w, p)
+    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
+    _assert_same(g, o, f"bid minima win {win} {case}")
+    _assert_same(g2, o, f"bid minima win {win} {case}, second solve")
+
+
 def test_csr_scan_many_nodes(oracle):
     """More than one 65,536-node tile in the node scan of the counting-mode
     bidder index (running carry between tiles)."""
@@ -1015,3 +1042,78 @@ def test_golden_fixture_gpu(name):
     for k in ("node", "score", "status", "used"):
         assert np.array_equal(g[k], z["out_" + k]), f"{name}: {k}"
     assert g["rounds"] == int(z["out_rounds"]) and g["passes"] == int(z["out_passes"]), name
+
+
+# ---------------------------------------------------------------------------
+# k_score32's class form (few capacity vectors) and kp_score_dev
+# ---------------------------------------------------------------------------
+def class_form_workload(seed, J, N, D=4, classes=3, wide=False):
+    """Node tables of `classes` capacity vectors (incl. a class with cap-0 dims)
+    in shuffled node order, usage anywhere in [0, cap], random requests:
+    k_score32's class form on every wave."""
+    rng = np.random.default_rng(seed)
+    top = (1 << 31) if wide else 64
+    shapes = rng.integers(1, top, size=(classes, D)).astype(np.int64)
+    shapes[0, D - 1] = 0  # a class with a cap-0 dim
+    cls = rng.integers(0, classes, size=N)
+    cap = np.ascontiguousarray(shapes[cls].T)
+    used = (cap * rng.random((D, N))).astype(np.int64)
+    full = rng.random(N) < 0.05
+    used[:, full] = cap[:, full]
+    req = (rng.integers(0, max(2, top // 4), size=(D, J))).astype(np.int64)
+    req[:, rng.random(J) < 0.05] = 0
+    topo = (np.arange(N) // 7).astype(np.int32)
+    aff = np.where(rng.random(J) < 0.3, rng.integers(0, N // 7 + 1, size=J), -1).astype(np.int32)
+    return synth.Workload(J, N, D, np.ascontiguousarray(req), cap, used,
+                          np.zeros(J, np.int32), np.full(J, -1, np.int32), np.ones(J, np.int32),
+                          topo, name=f"fewcls{seed}", affinity=aff)
+
+
+@pytest.mark.parametrize("classes,mode,scale,wide", [(1, 0, 100, False), (3, 1, 100, False),
+                                                     (8, 0, 1024, False), (5, 1, 7, True),
+                                                     (9, 0, 100, False)])
+def test_score_matrix_class_form(oracle, monkeypatch, classes, mode, scale, wide):
+    """kp_score through the class form (<= 8 capacity classes; 9 takes the
+    per-wave form) equals the oracle's kpo_score, and the per-wave form
+    (KP_SCORE_CLASSES=0) agrees; timing reports which form ran."""
+    w = class_form_workload(classes * 7 + mode, J=257, N=1111, classes=classes, wide=wide)
+    p = _abi.default_params(score_mode=mode, util_scale=scale)
+    osc, omk = oracle.score(oracle.SnapshotBuf(w.req, w.cap, w.used, topo=w.topo,
+                                               affinity=w.affinity), p, 0, w.J)
+    for knob in ("1", "0"):
+        monkeypatch.setenv("KP_SCORE_CLASSES", knob)
+        with Placer(device=0) as pl:
+            pl.load_nodes(w.cap, w.used, w.topo)
+            pl.load_jobs(w.req, affinity=w.affinity)
+            sc, mk = pl.score(p, 0, w.J)
+        assert np.array_equal(sc, osc), f"classes {classes} knob {knob}"
+        assert np.array_equal(mk, omk), f"classes {classes} knob {knob}"
+
+
+@pytest.mark.parametrize("cfg", [(2, 3_000, 1_000), (3, 4_000, 1_500), (4, 3_000, 2_000)])
+def test_score_dev_parity(oracle, cfg):
+    """kp_score_dev into torch-owned device buffers (padded rows of
+    round_up(N, 64)): the first N columns equal the oracle's matrix and mask,
+    padding columns are infeasible / zero bits; profiling reports the class
+    form and algorithmic bytes."""
+    from kplace.devmem import DeviceBuffer
+    no, J, N = cfg
+    w = synth.config(no, J, N)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[no])
+    Ns = (N + 63) // 64 * 64
+    lo, hi = 17, J - 5
+    with DeviceBuffer((hi - lo) * Ns * 4, fill=0x5A) as sc, \
+            DeviceBuffer((hi - lo) * (Ns // 64) * 8, fill=0x5A) as mk:
+        with Placer(device=0) as pl:
+            pl.load_nodes(w.cap, w.used, w.topo)
+            pl.load_jobs(w.req, w.prio, w.gang_id, w.gang_size)
+            pl.set_profiling(True)
+            pl.score_dev(p, lo, hi, sc.ptr, mk.ptr)
+            t = pl.timing()
+        g = sc.to_numpy(np.int32, (hi - lo, Ns))
+        gm = mk.to_numpy(np.uint64, (hi - lo, Ns // 64))
+    osc, omk = oracle.score(_snap(oracle, w), p, lo, hi)
+    assert np.array_equal(g[:, :N], osc) and (g[:, N:] == -1).all()
+    assert np.array_equal(gm[:, :omk.shape[1]], omk)
+    assert t["score_form"] == 1 and t["score_classes"] >= 1 and t["score_bytes"] > (hi - lo) * Ns * 4
+    assert t["score_ms"] > 0

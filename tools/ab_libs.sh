@@ -5,10 +5,10 @@
 set -o pipefail
 mkdir -p gpurun_out/ab
 LIBS=${LIBS:-"lib $(ls ab/*.so 2>/dev/null | grep -v passprof)"}
-for i in 1 2 3; do
+for i in $(seq 1 ${ITER:-3}); do
   for lib in $LIBS; do
     if [ "$lib" = lib ]; then n=lib; L=; else n=$(basename $lib .so); L=$PWD/$lib; fi
-    KPLACE_LIB=$L timeout -k 10 120 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-stream --no-config4 --place-steps 0 --no-kernel-events --out gpurun_out/ab/$n.$i.json > gpurun_out/ab/$n.$i.log 2>&1 || exit $?
+    KPLACE_LIB=$L timeout -k 10 120 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-stream --no-config4 --place-steps 0 --no-kernel-events --no-score-matrix --out gpurun_out/ab/$n.$i.json > gpurun_out/ab/$n.$i.log 2>&1 || exit $?
     python3 -c "import json;b=json.load(open('gpurun_out/ab/$n.$i.json'));print('$n', round(b['ms_per_step'],3), b['config']['rounds'], b['config']['passes'], b['config']['placed_jobs'])"
     if [ "$C4" = 1 ]; then KPLACE_LIB=$L timeout -k 10 300 python3 tools/c4_time.py || exit $?; fi
   done

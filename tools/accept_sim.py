@@ -9,6 +9,9 @@ critical path is the node with the most levels.
 
   KPO_DUMP=/tmp/c3.dump python tools/round_shape.py 3 > /dev/null
   python tools/accept_sim.py /tmp/c3.dump 3
+  TAIL=1 ...: per pass, the node with the most decided windows (the tail of the
+  launch): its bidder entries, windows, flagged windows, windows that pass the
+  window-minimum test (decided), windows with a bidder that fits, accepted bids
 """
 import ctypes as C
 import os
@@ -94,6 +97,32 @@ def main():
             bidmin = bidmin.reshape(D, nwin, 64).min(axis=2)
             worst = {k: 0 for k in MODES}
             bid_nodes = np.unique(props[:, 1])
+            if os.environ.get("TAIL"):
+                tail = None
+                for n in bid_nodes:
+                    i = np.searchsorted(nodes, n)
+                    e0, e1 = starts[i], starts[i] + counts[i]
+                    rem = w.cap[:, n] - used[:, n]
+                    dec = fitw = acc = nfl = 0
+                    for x in range(e0 // 64, (e1 - 1) // 64 + 1):
+                        if not flag[x]:
+                            continue
+                        nfl += 1
+                        if not (winmin[:, x] <= rem).all():
+                            continue
+                        dec += 1
+                        lo, hi = max(x * 64, e0), min(x * 64 + 64, e1)
+                        any_fit = False
+                        for ee in range(lo, hi):
+                            if m[ee] and (need[:, ee] <= rem).all():
+                                rem = rem - need[:, ee]
+                                acc += 1
+                                any_fit = True
+                        fitw += any_fit
+                    if tail is None or dec > tail[4]:
+                        tail = (n, e1 - e0, (e1 - 1) // 64 - e0 // 64 + 1, nfl, dec, fitw, acc)
+                print(f"  pass: node {tail[0]} entries {tail[1]} windows {tail[2]} flagged {tail[3]} "
+                      f"decided {tail[4]} with-fit {tail[5]} accepted {tail[6]}", flush=True)
             for n in bid_nodes:
                 i = np.searchsorted(nodes, n)
                 e0, e1 = starts[i], starts[i] + counts[i]

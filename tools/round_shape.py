@@ -3,7 +3,7 @@
 candidate nodes (the bid-node bound), the longest bidder row, unit sizes and the
 passes the round ran. Sizes the one-workgroup LDS round kernel.
 
-  python tools/round_shape.py [config_no] [J] [N]
+  python tools/round_shape.py [config_no] [J] [N]     (MAXR=r: the first r rounds only)
 """
 import ctypes as C
 import os
@@ -33,7 +33,8 @@ def main():
     r = 0
     print("round      A    A*K  nodes  maxrow  size>1  passes")
     tot_p = 0
-    while L.kpo_state_active(st) > 0:
+    maxr = int(os.environ.get("MAXR", "0"))
+    while L.kpo_state_active(st) > 0 and not (maxr and r >= maxr):
         cand[:] = -1
         L.kpo_round_candidates(st, 0, U, cand.ctypes.data_as(C.POINTER(C.c_int32)), os.cpu_count())
         act = cand[:, 0] >= 0
