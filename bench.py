@@ -292,7 +292,19 @@ def score_matrix(args, make_placer, w, p):
     mk.close()
     gbs = (by / 1e9) / (ms / 1e3) if ms > 0 else 0.0
     pairs = float(w.J) * w.N * args.score_steps
+    kname = "k_score32c" if tm["score_form"] == 1 else "k_score32"
+    traffic, traffic_src = None, None
+    for pmc in ("r04_pmc.json",):  # HBM-side bytes per launch of this kernel (rocprofv3 PMC)
+        path = os.path.join(REPO, "profiles", pmc)
+        if os.path.exists(path):
+            with open(path) as f:
+                k = [v for n, v in json.load(f)["kernels"].items() if n.startswith(kname + "<") or n == kname]
+            if k:
+                traffic = k[0]["traffic_bytes_per_launch"] * (ln / max(args.score_steps, 1))
+                traffic_src = f"profiles/{pmc} (FETCH_SIZE x2 + WRITE_SIZE per launch x launches per call)"
+                break
     return {"kernel": "k_score32c (capacity-class form)" if tm["score_form"] == 1 else "k_score32",
+            "traffic": traffic, "traffic_source": traffic_src,
             "entry": "kp_score_dev", "rows": w.J, "nodes": w.N, "row_stride": Ns,
             "capacity_classes": tm["score_classes"], "calls": args.score_steps,
             "launches_per_call": ln / max(args.score_steps, 1),
@@ -468,7 +480,7 @@ def main():
     fused = bool(tm["fused"])
     kname = "k_score_topk" if fused else "k_score32"
     traffic, traffic_src, valu = None, None, None
-    for pmc in ("r03_pmc.json", "r02_pmc.json", "r01_pmc.json"):  # HBM-side bytes per launch (rocprofv3 PMC), newest first
+    for pmc in ("r04_pmc.json", "r03_pmc.json", "r02_pmc.json", "r01_pmc.json"):  # HBM-side bytes per launch (rocprofv3 PMC), newest first
         path = os.path.join(REPO, "profiles", pmc)
         if os.path.exists(path):
             with open(path) as f:
@@ -483,7 +495,7 @@ def main():
         # judged on pairs/s and on the VALU roofline (lane-ops per pair from
         # the SQ_INSTS_VALU counter of the same solve, profiles/r0N_valu.json)
         opp, vsrc = None, None
-        for vj in ("r03_valu.json", "r02_valu.json"):  # newest evidence first
+        for vj in ("r04_valu.json", "r03_valu.json", "r02_valu.json"):  # newest evidence first
             path = os.path.join(REPO, "profiles", vj)
             if os.path.exists(path):
                 with open(path) as f:

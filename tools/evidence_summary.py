@@ -40,6 +40,8 @@ copy("pytest_gpu.log", "pytest_gpu.log")
 copy("bench.json", "bench.json")
 copy("prof/run_kernel_stats.csv", "kernel_stats.csv")
 copy("prof/bench_prof.json", "bench_profiled_cmd.json")
+copy("profsm/run_kernel_stats.csv", "kernel_stats_score_matrix.csv")
+copy("profsm/score_dev.log", "score_dev_profiled.txt")
 copy("prof45/run_kernel_stats.csv", "kernel_stats_config4_config5.csv")
 copy("prof45/bench_prof.json", "bench_profiled_config4_config5.json")
 

@@ -9,7 +9,7 @@
 #   6. a HIP runtime trace of kp_place calls (hipMalloc / hipFree inside steps)
 set -o pipefail
 OUT=gpurun_out/evidence
-rm -rf $OUT; mkdir -p $OUT/prof $OUT/prof45 $OUT/pmc $OUT/rt
+rm -rf $OUT; mkdir -p $OUT/prof $OUT/profsm $OUT/prof45 $OUT/pmc $OUT/rt
 rocminfo 2>/dev/null | grep -m1 gfx950 > $OUT/arch.txt || true
 if [ "$SKIP_TESTS" != 1 ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
@@ -20,9 +20,12 @@ if [ "$SKIP_BENCH" != 1 ]; then
   echo bench ok
 fi
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-B3="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-stream --no-config4 --place-steps 0"
+B3="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-stream --no-config4 --place-steps 0 --no-score-matrix"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $B3 --out $OUT/prof/bench_prof.json > $OUT/prof/bench.log 2>&1 || exit $?
 echo prof ok
+# the materialised score matrix + mask (kp_score_dev, config #3 full queue) on its own
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsm -o run -- python3 tools/score_dev_time.py > $OUT/profsm/score_dev.log 2>&1 || exit $?
+echo profsm ok
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof45 -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --place-steps 0 --c4-steps 1 --out $OUT/prof45/bench_prof.json > $OUT/prof45/bench.log 2>&1 || exit $?
 echo prof45 ok
 B1="bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-stream --no-config4 --place-steps 0"
@@ -49,7 +52,7 @@ if [ -f $NOSEL ]; then
 fi
 timeout -k 10 300 rocprofv3 --hip-runtime-trace --kernel-trace --output-format csv -d $OUT/rt -o run -- python3 tools/place_steps.py > $OUT/rt/place.log 2>&1 || exit $?
 echo rt ok
-python3 tools/evidence_summary.py ${ROUND:-r03} $OUT $OUT/summary && ls $OUT/summary
+python3 tools/evidence_summary.py ${ROUND:-r04} $OUT $OUT/summary && ls $OUT/summary
 # the raw traces exceed what gpurun copies back: keep logs and summaries only
-rm -f $OUT/prof/run_kernel_trace.csv $OUT/prof45/run_kernel_trace.csv $OUT/*/*/run_counter_collection.csv $OUT/*/*/run_kernel_trace.csv
+rm -f $OUT/prof/run_kernel_trace.csv $OUT/profsm/run_kernel_trace.csv $OUT/prof45/run_kernel_trace.csv $OUT/*/*/run_counter_collection.csv $OUT/*/*/run_kernel_trace.csv
 du -sh $OUT
