@@ -15,11 +15,17 @@ Beside the step (same run, outside the timed steps):
                   placement latency"; the reference's analogue is
                   the reconcile histogram around Reconcile,
                   internal/controller/llmservice_controller.go:70-73);
+  phases          one extra solve with per-round phase events: candidate
+                  phase / candidate exchange / passes (max over ranks);
+  score_matrix    the materialised int32 score matrix + feasibility bitmask
+                  of the whole queue (kp_score_dev; on N GPUs each rank its
+                  row block) against the HBM roofline;
   config4         BASELINE config #4 (200k x 20k, running jobs filling every
-                  dim to >= 30% of its capacity): solve + kp_preempt, with the
-                  oracle timed beside it on a stated sample;
+                  dim to >= 30% of its capacity): solve + kp_preempt on the
+                  same N GPUs (row-sharded, collective), with its phase split
+                  and, at N = 1, the oracle timed beside it on a stated sample;
   streaming       BASELINE config #5 (1M-job trace, 5k micro-batches, 50k nodes),
-                  with the oracle timed beside it on the first batches;
+                  with the oracle timed beside it on the first batches (N = 1);
   cpu_baseline    the CPU restatement (oracle/, test infrastructure) on the SAME
                   full config #3, on 1 thread and on every host core given to
                   this job.
@@ -228,10 +234,36 @@ def config4_cpu(args, w, p):
                       f"pairs of the solve + preemption", **out}
 
 
-def config4(args, make_placer):
+def phase_split(pl, p, sync=lambda x: x, gather=lambda d: [d]) -> dict:
+    """One extra solve (after the timed steps, from the same reset snapshot)
+    with the per-round phase events on (kp_set_profiling level 2): candidate
+    phase (round start + filter/score/top-K + merge), candidate exchange
+    (pack + all-gather + unpack; multi-rank only), passes (bidder index +
+    plan/accept + commit), summed over the rounds. Per rank; `value` fields
+    are the max over ranks."""
+    pl.reset_nodes()
+    pl.set_profiling(2)
+    st = pl.solve(p)
+    tm = pl.timing()
+    pl.set_profiling(False)
+    mine = {"solve_ms": tm["solve_ms"], "cand_ms": tm["cand_ms"], "xchg_ms": tm["xchg_ms"],
+            "pass_ms": tm["pass_ms"], "rounds": st["rounds"]}
+    ranks = gather(mine)
+    out = {k: max(r[k] for r in ranks) for k in ("solve_ms", "cand_ms", "xchg_ms", "pass_ms")}
+    out.update(rounds=st["rounds"], per_rank=ranks,
+               note="device time from HIP events at each round's phase boundaries (their own "
+                    "records add a few us per round); max over ranks")
+    return out
+
+
+def config4(args, make_placer, n_gpus=1, barrier=lambda: None, max_over_ranks=lambda x: x,
+            gather=lambda d: [d]):
     """BASELINE config #4: 200k pending x 20k nodes pre-filled with running
     jobs (priorities 0-3) to 30% GPU occupancy; one step = reset the resident
-    usage + solve + preemption nominations for every NO_FIT singleton."""
+    usage + solve + preemption nominations for every NO_FIT singleton. On N
+    GPUs every rank runs the same calls (the solve and kp_preempt are
+    collective: row shards of the candidate phase and of the preemptors, one
+    all-gather per round / per preempt call); times are the max over ranks."""
     w = synth.config4(args.c4_jobs, args.c4_nodes)
     p = _abi.default_params(**synth.CONFIG_PARAMS[4])
     m = w.meta
@@ -243,46 +275,58 @@ def config4(args, make_placer):
         for it in range(args.c4_steps + 1):
             progress(f"config #4 step {it}")
             pl.reset_nodes()
+            barrier()
             t0 = time.perf_counter()
             st = pl.solve(p)
             t1 = time.perf_counter()
+            barrier()
+            t1b = time.perf_counter()
             pr = pl.preempt()
             t2 = time.perf_counter()
             if it:  # first iteration: warmup
-                sol.append(t1 - t0)
-                pre.append(t2 - t1)
+                sol.append(max_over_ranks(t1 - t0))
+                pre.append(max_over_ranks(t2 - t1b))
+        progress("config #4 phase split")
+        phases = phase_split(pl, p, gather=gather)
+        pl.reset_nodes()
+        phases["preempt_ms"] = 1e3 * float(np.mean(pre))
     s_ms, p_ms = 1e3 * float(np.mean(sol)), 1e3 * float(np.mean(pre))
     util = w.used.sum(1) / w.cap.sum(1)
-    cpu = None if args.no_cpu_baseline else config4_cpu(args, w, p)
+    cpu = None if args.no_cpu_baseline or n_gpus > 1 else config4_cpu(args, w, p)
     return {"config": f"#4 preemption: {w.J} pending x {w.N} nodes, {m['run_node'].size} running "
                       f"jobs; occupancy per dim (cpu, mem, gpu, gpu_mem) "
                       f"{', '.join(f'{x:.3f}' for x in util)} (every dim >= 0.30)",
+            "n_gpus": n_gpus,
             "solve_ms": s_ms, "preempt_ms": p_ms,
             "pairs_per_s": float(w.J) * w.N / ((s_ms + p_ms) / 1e3),
             "pairs_scored_per_s": (float(st["pairs"]) + float(pr["pairs"])) / ((s_ms + p_ms) / 1e3),
             "cpu_baseline": cpu,
             "rounds": st["rounds"], "passes": st["passes"], "placed_jobs": st["placed"],
             "preemptors": pr["preemptors"], "nominated": pr["nominated"],
-            "preempt_pairs": pr["pairs"], "steps": args.c4_steps}
+            "preempt_pairs": pr["pairs"], "steps": args.c4_steps, "phases": phases}
 
 
-def score_matrix(args, make_placer, w, p):
+def score_matrix(args, make_placer, w, p, rank=0, world=1, gather=lambda d: [d]):
     """The materialised filter + score outputs north_star names (int32 score
     matrix + feasibility bitmask) for the WHOLE config #3 queue, written into
-    HBM by kp_score_dev (k_score32's capacity-class form): HIP-event kernel
+    HBM by kp_score_dev (k_score32c, the capacity-class form): HIP-event kernel
     time and algorithmic bytes (outputs once + requests + node planes) from
-    kp_last_timing, against the HBM peak."""
+    kp_last_timing, against the HBM peak. On N GPUs (one process per GPU) each
+    rank scores its contiguous block of rows on its own GPU (a one-GPU
+    context: no exchange is needed); aggregate = all ranks' bytes / the
+    slowest rank's kernel time."""
     from kplace.devmem import DeviceBuffer  # libkplace's own HIP runtime (not torch's)
     Ns = (w.N + 63) // 64 * 64
-    sc = DeviceBuffer(w.J * Ns * 4)
-    mk = DeviceBuffer(w.J * (Ns // 64) * 8)
+    lo, hi = w.J * rank // world, w.J * (rank + 1) // world
+    sc = DeviceBuffer((hi - lo) * Ns * 4)
+    mk = DeviceBuffer((hi - lo) * (Ns // 64) * 8)
     ms, by, ln, tm = 0.0, 0, 0, None
     with make_placer() as pl:
         pl.load_nodes(w.cap, w.used, w.topo)
         pl.load_jobs(w.req, w.prio, w.gang_id, w.gang_size)
         pl.set_profiling(True)
         for it in range(args.score_steps + 1):
-            pl.score_dev(p, 0, w.J, sc.ptr, mk.ptr)
+            pl.score_dev(p, lo, hi, sc.ptr, mk.ptr)
             tm = pl.timing()
             if it:  # first call: warmup
                 ms += tm["score_ms"]
@@ -290,26 +334,31 @@ def score_matrix(args, make_placer, w, p):
                 ln += tm["score_launches"]
     sc.close()
     mk.close()
+    ranks = gather({"ms": ms, "bytes": by, "launches": ln, "rows": hi - lo})
+    ms = max(r["ms"] for r in ranks)
+    by = sum(r["bytes"] for r in ranks)
+    ln = ranks[0]["launches"]
     gbs = (by / 1e9) / (ms / 1e3) if ms > 0 else 0.0
     pairs = float(w.J) * w.N * args.score_steps
     kname = "k_score32c" if tm["score_form"] == 1 else "k_score32"
     traffic, traffic_src = None, None
-    for pmc in ("r04_pmc.json",):  # HBM-side bytes per launch of this kernel (rocprofv3 PMC)
+    for pmc in ("r05_pmc.json", "r04_pmc.json"):  # HBM-side bytes per launch (rocprofv3 PMC), newest first
         path = os.path.join(REPO, "profiles", pmc)
         if os.path.exists(path):
             with open(path) as f:
                 k = [v for n, v in json.load(f)["kernels"].items() if n.startswith(kname + "<") or n == kname]
-            if k:
+            if k and world == 1:
                 traffic = k[0]["traffic_bytes_per_launch"] * (ln / max(args.score_steps, 1))
                 traffic_src = f"profiles/{pmc} (FETCH_SIZE x2 + WRITE_SIZE per launch x launches per call)"
                 break
     return {"kernel": "k_score32c (capacity-class form)" if tm["score_form"] == 1 else "k_score32",
             "traffic": traffic, "traffic_source": traffic_src,
-            "entry": "kp_score_dev", "rows": w.J, "nodes": w.N, "row_stride": Ns,
+            "entry": "kp_score_dev", "rows": w.J, "nodes": w.N, "row_stride": Ns, "n_gpus": world,
+            "rows_per_rank": [r["rows"] for r in ranks],
             "capacity_classes": tm["score_classes"], "calls": args.score_steps,
             "launches_per_call": ln / max(args.score_steps, 1),
-            "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": gbs / HBM_PEAK_GBS, "bytes_per_call": by / max(args.score_steps, 1),
+            "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+            "frac": gbs / (HBM_PEAK_GBS * world), "bytes_per_call": by / max(args.score_steps, 1),
             "ms_per_call": ms / max(args.score_steps, 1), "pairs_per_s": pairs / (ms / 1e3) if ms else 0.0,
             "algorithmic_bytes": "rows x Ns x 4 (scores) + rows x Ns / 8 (mask) + rows x (8D + 4) "
                                  "(requests) + (2D + 4) x 4 x Ns (node planes)"}
@@ -386,11 +435,22 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
-    nid = None
-    if world > 1 and args.exchange == "rccl":
+    def fresh_id():
+        """A new RCCL unique id for every multi-rank context (an id
+        bootstraps one communicator), broadcast from rank 0 over gloo."""
+        if world == 1 or args.exchange != "rccl":
+            return None
         obj = [unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        nid = obj[0]
+        return obj[0]
+
+    def gather(d: dict) -> list:
+        """Every rank's dict, rank order (rank 0 reports them)."""
+        if dist is None:
+            return [d]
+        out = [None] * world
+        dist.all_gather_object(out, d)
+        return out
 
     rehearsal = False
     if args.single_process:
@@ -399,6 +459,7 @@ def main():
             sys.exit(f"bench.py: --gpus {args.gpus} but --gpu-ids names {len(ids)} GPUs")
         rehearsal = len(set(ids)) < len(ids)
         make_placer = lambda: Placer(gpu_ids=ids)  # noqa: E731
+        make_local = None  # kp_score_dev needs a one-GPU context
         parallelism = f"job-row shards x{args.gpus} (one process, kp_create_multi)"
         n_gpus = args.gpus
     elif world > 1 and args.exchange == "host":
@@ -414,11 +475,13 @@ def main():
         rehearsal = True
         make_placer = lambda: Placer(device=dev, world_size=world, rank=rank,  # noqa: E731
                                      allgather=allgather)
+        make_local = lambda: Placer(device=dev)  # noqa: E731
         parallelism = f"job-row shards x{world} (host-staged exchange)"
         n_gpus = world
     else:
         make_placer = lambda: Placer(device=local, world_size=world, rank=rank,  # noqa: E731
-                                     nccl_id=nid)
+                                     nccl_id=fresh_id())
+        make_local = lambda: Placer(device=local)  # noqa: E731  (a one-GPU context on this rank's GPU)
         parallelism = f"job-row shards x{world}"
         n_gpus = world
 
@@ -460,6 +523,10 @@ def main():
     dt = max_over_ranks(time.perf_counter() - t0)
     ms = dt * 1e3 / args.steps
     pl.set_profiling(False)
+    # where a solve's time goes (outside the timed steps): candidate phase /
+    # exchange / passes, max over ranks
+    progress("phase split")
+    phases = phase_split(pl, p, gather=gather)
 
     # full-queue placement latency: snapshot in host memory -> assignment in
     # host memory (kp_place: validate + H2D + solve + D2H), outside the steps
@@ -472,6 +539,23 @@ def main():
     pl.close()
     latency_ms = 1e3 * float(np.median(lat)) if lat else None
 
+    # the other legs: every rank runs the collective ones (config #4 solve +
+    # kp_preempt on N GPUs); the streaming leg (latency-bound 5k-job batches)
+    # and the CPU baselines run at N = 1 only
+    legs = {}
+    if not args.no_score_matrix and (n_gpus == 1 or make_local is not None):
+        progress("score matrix leg")
+        legs["score_matrix"] = score_matrix(args, make_local if n_gpus > 1 else make_placer, w, p,
+                                            rank=rank, world=world, gather=gather)
+    if not args.no_config4:
+        progress("config #4 leg")
+        legs["config4"] = config4(args, make_placer, n_gpus, barrier, max_over_ranks, gather)
+    if not args.no_stream and n_gpus == 1:
+        progress("config #5 streaming leg")
+        legs["streaming"] = streaming(args, make_placer)
+    if not args.no_cpu_baseline and n_gpus == 1:
+        progress("cpu baseline leg")
+        legs["cpu_baseline"] = cpu_baseline(args, w, p)
     if rank != 0:
         dist.barrier()
         return
@@ -549,19 +633,9 @@ def main():
                      "launches_per_step": launches / args.steps,
                      "avg_launch_ms": score_ms / max(launches, 1),
                      "valu": valu},
+        "phases": phases,
     }
-    if not args.no_score_matrix and n_gpus == 1:
-        progress("score matrix leg")
-        out["score_matrix"] = score_matrix(args, make_placer, w, p)
-    if not args.no_config4 and n_gpus == 1:
-        progress("config #4 leg")
-        out["config4"] = config4(args, make_placer)
-    if not args.no_stream and n_gpus == 1:
-        progress("config #5 streaming leg")
-        out["streaming"] = streaming(args, make_placer)
-    if not args.no_cpu_baseline and n_gpus == 1:
-        progress("cpu baseline leg")
-        out["cpu_baseline"] = cpu_baseline(args, w, p)
+    out.update(legs)
     line = json.dumps(out)
     print(line, flush=True)
     if args.out:

@@ -33,8 +33,13 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 6  /* 4: kp_last_error_r; 5: kp_timing.incr_rounds;
-                              6: kp_score_dev, kp_timing.score_form / score_classes */
+#define KP_ABI_VERSION 7  /* 4: kp_last_error_r; 5: kp_timing.incr_rounds;
+                              6: kp_score_dev, kp_timing.score_form / score_classes;
+                              7: kp_timing phase split (cand/xchg/pass_ms,
+                                 kp_set_profiling level 2); kp_load_running and
+                                 kp_preempt are collective on world_size > 1
+                                 contexts (every rank calls them, in the same
+                                 order as its kp_solve calls) */
 
 /* ---- limits ------------------------------------------------------------ */
 #define KP_MAX_DIMS 8       /* resource dimensions per job/node               */
@@ -246,6 +251,13 @@ int kp_score_dev(kp_ctx *ctx, const kp_params *p, int32_t job_lo, int32_t job_hi
  * job r uses req[d*R + r] on node[r] with priority prio[r]; its usage must
  * already be part of the loaded `used` (per node and dim the running requests
  * sum to <= used), else KP_EINVAL. kp_load_nodes clears the pool.
+ *
+ * COLLECTIVE on a multi-process context (kp_create with world_size > 1):
+ * every rank loads the whole pool, and kp_preempt scores its own block of the
+ * preemptor list and all-gathers the nominations, so every
+ * rank must call kp_load_running and kp_preempt, like kp_solve; a call on one
+ * rank alone blocks in the exchange. kp_create_multi contexts drive their
+ * shards themselves (one call from the host).
  */
 int kp_load_running(kp_ctx *ctx, int32_t R, const int32_t *node, const int64_t *req,
                     const int32_t *prio);
@@ -274,7 +286,10 @@ int kp_preempt(kp_ctx *ctx, kp_preemption *out);
 /* Timing of the last kp_solve, measured with HIP events on the solve stream
  * (kp_set_profiling(ctx, 1)): the filter+score launches are bracketed; the
  * select is not (select_ms = 0, select_bytes still counted) and accept_ms is
- * the rest of the solve. */
+ * the rest of the solve. Level 2 (kp_set_profiling(ctx, 2)) adds event records
+ * at every round's phase boundaries (a few us each: diagnosis, not the timed
+ * steps) and fills the phase split; the phases sum to solve_ms up to the
+ * solve's first and last launches. */
 typedef struct kp_timing {
   double solve_ms;          /* whole device solve (first launch .. last)     */
   double score_ms;          /* sum of filter+score kernel time               */
@@ -291,12 +306,20 @@ typedef struct kp_timing {
   int32_t score_classes;    /* capacity classes of the node table (0: more than
                                the class form handles) */
   int32_t pad;
+  /* level 2 only (else 0), summed over the solve's rounds: */
+  double cand_ms;           /* candidate phase: round start (active-unit
+                               compaction, node pack) + filter/score/top-K +
+                               candidate merge of this rank's units          */
+  double xchg_ms;           /* candidate exchange of a multi-rank solve: pack
+                               + all-gather + unpack (0 on one GPU)          */
+  double pass_ms;           /* bidder index + plan/accept passes + commit    */
 } kp_timing;
 int kp_last_timing(kp_ctx *ctx, kp_timing *t);
 
-/* Enable/disable per-kernel HIP-event timing (off by default: it adds
-   event records between launches). */
-int kp_set_profiling(kp_ctx *ctx, int enable);
+/* HIP-event timing: 0 off (default), 1 the filter+score launches, 2 also the
+   per-round phase split (kp_timing.cand/xchg/pass_ms). Both add event records
+   between launches. */
+int kp_set_profiling(kp_ctx *ctx, int level);
 
 /* Host-side helper for the snapshot packer: parses an LLMService GPUMemory
    string (CRD pattern ^\d+(Gi|Mi)$, ai.ruijie.io_llmservices.yaml:48-51) into

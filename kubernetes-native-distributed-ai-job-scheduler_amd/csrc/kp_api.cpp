@@ -19,6 +19,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
@@ -853,6 +854,17 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   KP_HIP(hipEventRecord(t0, c->stream));
   std::vector<int32_t> round_active;  // exact active units per round (when known)
   kp_timing tm{};
+  // profiling level 2: per round, events at the round start, after the
+  // candidate phase, after the exchange (multi-rank) and after the passes
+  std::vector<std::array<hipEvent_t, 4>> pev;
+  auto mark = [&](int i) -> int {
+    if (c->profiling < 2) return KP_OK;
+    if (i == 0) pev.push_back({nullptr, nullptr, nullptr, nullptr});
+    if (pev.empty()) return KP_OK;
+    KP_TRY(E.make(&pev.back()[i], hipEventDisableSystemFence));
+    KP_HIP(hipEventRecord(pev.back()[i], c->stream));
+    return KP_OK;
+  };
   // filter+score and top-K select of `rows` rows starting at act_local[r0];
   // rows_dev (nullable) clamps them to the device count
   auto score_select = [&](int64_t r0, int32_t rows, const int32_t *rows_dev,
@@ -1010,6 +1022,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     for (int32_t r = 0; A_bound > 0; ++r) {
       if (p->max_rounds > 0 && r >= p->max_rounds) break;
       KP_TRY(next_serial());
+      KP_TRY(mark(0));
       bool direct = true;
       KP_TRY(launch_active_async(c, c->u_lo, c->u_hi, A_h, &direct));
       if (!direct) KP_HIP(hipEventRecord(evA, c->stream));
@@ -1019,14 +1032,18 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
         if (A == 0) break;
         for (int64_t r0 = 0; r0 < A; r0 += rpc)
           KP_TRY(score_select(r0, (int32_t)std::min<int64_t>(rpc, A - r0), nullptr, r));
+        KP_TRY(mark(1));
         round_active.push_back(A);
         KP_TRY(passes_of_round(A, nullptr, true));
+        KP_TRY(mark(3));
         A_bound = A;
         continue;
       }
       const int32_t *A_dev = c->d.counters;
       KP_TRY(score_select(0, (int32_t)A_bound, A_dev, r));
+      KP_TRY(mark(1));
       KP_TRY(passes_of_round((int32_t)A_bound, A_dev, true));
+      KP_TRY(mark(3));
       KP_TRY(round_count(direct));  // landed long ago on a busy round
       round_active.push_back(*A_h);
       A_bound = *A_h;
@@ -1061,6 +1078,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     for (int32_t r = 0; G_bound > 0; ++r) {
       if (p->max_rounds > 0 && r >= p->max_rounds) break;
       KP_TRY(next_serial());
+      KP_TRY(mark(0));
       const int32_t B = (int32_t)std::min<int64_t>(Smax, G_bound);  // per-rank slot bound
       if (shard > 0) {
         KP_TRY(launch_active_async(c, c->u_lo, c->u_hi, Al_h));
@@ -1080,12 +1098,15 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
         c->test_fail_solve = 0;
         return fail(KP_ENOMEM, "KP_TEST_FAIL_SOLVE: injected failure of rank %d before its exchange", c->rank);
       }
+      KP_TRY(mark(1));
       KP_TRY(exchange_round(c, B, K));
+      KP_TRY(mark(2));
       KP_HIP(hipMemcpyAsync(G_h, c->d.counters + 1, sizeof(int32_t), hipMemcpyDeviceToHost,
                             c->stream));
       KP_HIP(hipEventRecord(evG, c->stream));
       KP_TRY(passes_of_round((int32_t)std::min<int64_t>(U, (int64_t)B * c->world),
                              c->d.counters + 1, true));
+      KP_TRY(mark(3));
       KP_TRY(wait_event(c, evG));  // lands before this round's passes run
       round_active.push_back(*Al_h);
       G_bound = *G_h;
@@ -1133,6 +1154,12 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     }
   }
   tm.accept_ms = tm.solve_ms - tm.score_ms - tm.select_ms;
+  for (const auto &e : pev) {  // phase split (profiling level 2)
+    if (e[0] && e[1]) tm.cand_ms += ev_ms(e[0], e[1]);
+    if (e[1] && e[2]) tm.xchg_ms += ev_ms(e[1], e[2]);
+    const hipEvent_t from = e[2] ? e[2] : e[1];
+    if (from && e[3]) tm.pass_ms += ev_ms(from, e[3]);
+  }
   tm.fused = fused ? 1 : 0;
   tm.score_classes = c->n_classes;
   tm.score_form = !fused && c->fits32 && c->n_classes > 0 && c->score_classes ? 1 : 0;
@@ -1329,7 +1356,7 @@ void kp_destroy(kp_ctx *c) {
                   d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.pre_send, d.pre_recv, d.roff,
                   d.rreq, d.rsuf, d.rprio, d.pre_node, d.pre_vict, d.pre_cost,
                   d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.nrec, d.nst, d.stats, d.np32, d.ncls, d.ccap, d.colnode, d.wshift, d.part, d.fz_prof,
-                  d.bm, d.bms, d.rowinfo, d.cnt};
+                  d.bm, d.bms, d.rowinfo, d.cnt, d.rowmap};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->world > 1) {
@@ -1353,11 +1380,11 @@ int kp_set_allgather(kp_ctx *c, kp_allgather_fn fn, void *user) {
   return KP_OK;
 }
 
-int kp_set_profiling(kp_ctx *c, int enable) {
+int kp_set_profiling(kp_ctx *c, int level) {
   if (!c) return KP_EINVAL;
-  if (c->multi) return multi_run(c, [&](kp_ctx *sh, int) { return kp_set_profiling(sh, enable); }, true);
+  if (c->multi) return multi_run(c, [&](kp_ctx *sh, int) { return kp_set_profiling(sh, level); }, true);
   Entry en(c);
-  c->profiling = enable != 0;
+  c->profiling = level <= 0 ? 0 : std::min(level, 2);
   return KP_OK;
 }
 
@@ -1572,19 +1599,29 @@ int kp_score_dev(kp_ctx *c, const kp_params *p, int32_t job_lo, int32_t job_hi,
   c->pack_fused = false;
   c->pack_full = true;
   KP_TRY(launch_pack(c));
+  // one launch over every requested row (a row -> unit map of `rows` entries
+  // on the device): the grid's last partial wave of workgroups is paid once,
+  // not once per cap_U-row chunk (tools/score_roof.hip: 4 chunks cost 0.74 ->
+  // 0.78 ms of stores alone and more with the score arithmetic). Chunks only
+  // past the grid's y limit (65,535 row blocks of 64 rows).
+  if (c->cap_rowmap < rows) {
+    c->cap_rowmap = 0;
+    KP_TRY(dalloc(&c->d.rowmap, (size_t)rows));
+    c->cap_rowmap = rows;
+  }
+  KP_HIP(hipMemcpyAsync(c->d.rowmap, unit_of.data(), sizeof(int32_t) * rows, hipMemcpyHostToDevice,
+                        c->stream));
   Events E;
-  const int64_t chunk = std::max<int32_t>(c->cap_U, 1);
+  const int64_t chunk = (int64_t)65535 * 64;
   for (int64_t r0 = 0; r0 < rows; r0 += chunk) {
     const int32_t nr = (int32_t)std::min<int64_t>(chunk, rows - r0);
-    KP_HIP(hipMemcpyAsync(c->d.act_local, unit_of.data() + r0, sizeof(int32_t) * nr,
-                          hipMemcpyHostToDevice, c->stream));
     hipEvent_t a = nullptr, b = nullptr;
     if (c->profiling) {
       KP_TRY(E.make(&a, hipEventDisableSystemFence));
       KP_TRY(E.make(&b, hipEventDisableSystemFence));
       KP_HIP(hipEventRecord(a, c->stream));
     }
-    KP_TRY(launch_score(c, sp, c->d.act_local, nr, score_dev ? score_dev + r0 * Ns : nullptr,
+    KP_TRY(launch_score(c, sp, c->d.rowmap + r0, nr, score_dev ? score_dev + r0 * Ns : nullptr,
                         mask_dev ? mask_dev + r0 * words : nullptr, c->d.q, c->U));
     if (c->profiling) {
       KP_HIP(hipEventRecord(b, c->stream));

@@ -109,6 +109,7 @@ struct DevState {
   int32_t *cand_local = nullptr;// [U*K]
   int32_t *score = nullptr;     // [rows*N] materialised score matrix (chunk)
   uint64_t *mask = nullptr;     // [rows*ceil(N/64)]
+  int32_t *rowmap = nullptr;    // [rows] row -> unit of kp_score_dev's single launch
   uint8_t *open = nullptr;      // [U] per active slot
   int32_t *flag = nullptr;      // [U] active flags (compaction input)
   // pass state: per bidder entry e (node-sorted order) the pass-start score and
@@ -197,7 +198,7 @@ struct kp_ctx {
   int32_t test_fail_solve = 0;
   int64_t max_pairs_matrix = 0;
   hipStream_t stream = nullptr;
-  bool profiling = false;
+  int profiling = 0;  // kp_set_profiling level (0 off, 1 filter+score events, 2 + phase split)
   hipEvent_t fz_end_event = nullptr;  // profiling: recorded right after k_score_topk
   // test knobs, read from the environment at kp_create (never set in
   // production): KP_SELECT_LDS_CAP shrinks the threshold select's survivor
@@ -253,6 +254,7 @@ struct kp_ctx {
   bool fz_layout_ok = false, fused_enabled = true;
   int64_t max_cap = 0, max_req = 0;  // largest cap / request of the loaded tables
   int32_t cap_mask_rows = 0;   // rows of d.mask (kp_score only)
+  int64_t cap_rowmap = 0;      // entries of d.rowmap (kp_score_dev only)
   int64_t cap_q = 0;           // int64 entries of d.q
   int32_t u_lo = 0, u_hi = 0;  // this rank's shard of units (rank positions)
   bool nodes_loaded = false, jobs_loaded = false, solved = false;
@@ -309,6 +311,10 @@ int launch_prep_nodes(kp_ctx *c, int32_t S, int most_allocated, const int32_t *w
 // 32-bit node planes (d.np32) of the current usage; k_score32 reads them, so
 // every caller of launch_score packs first (the solve does it in the fused
 // round-start kernel of launch_active / launch_active_async)
+// order-preserving compaction of flags[0, n) into out (lo + index), count ->
+// counters[0] (and *host_count when given)
+int launch_compact_to(kp_ctx *c, const int32_t *flag, int32_t lo, int32_t n, int32_t *out,
+                      int32_t *host_count);
 int launch_pack(kp_ctx *c);
 // Kernels that take a device count pointer (rows_dev / A_dev, nullable) size
 // their grid by the host bound and clamp to the device count, so a round can

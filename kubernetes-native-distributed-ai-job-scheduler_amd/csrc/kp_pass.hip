@@ -642,30 +642,49 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
     }
     return;
   }
+  // Long rows (k_csr_place, >= KP_BMIN_WIN windows): the window's smallest
+  // bid of this pass per dim — tighter than the round's smallest request,
+  // so accept skips, unread, the windows of a herded row none of whose
+  // bids of this pass fits (config #4's tail); the pass tag in the high
+  // bits makes atomicMax keep this pass's minimum. The wave's bids are
+  // pre-reduced per window first (consecutive slots bid into the same
+  // windows of a herded row): one atomic per window and dim instead of one
+  // per bid (the same-address atomics serialise at the L2 and the launch
+  // ends only when they have drained). Short rows only flag the window (one
+  // plain store: atomics for every bid cost a config #3 solve ~2.3 ms),
+  // which also tells accept the bid minima do not bound every bid of the
+  // window.
+  {
+    const bool lr = prop && inv_raw < 0;
+    uint64_t pend = __ballot(lr);  // over the lanes still running (whole groups)
+    const uint64_t tag = (uint64_t)(pass + 1) << 48, lo = (1ull << 48) - 1;
+    while (pend) {  // wave-uniform: once per distinct window of the wave's long-row bids
+      const int ld = __ffsll((unsigned long long)pend) - 1;
+      const int32_t wk = __builtin_amdgcn_readlane(e_inv >> 6, ld);
+      const uint64_t grp = __ballot(lr && (e_inv >> 6) == wk);
+      pend &= ~grp;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const uint64_t need = (uint64_t)planned * (uint64_t)qq[d];
+        const uint32_t nlo = (uint32_t)need, nhi = (uint32_t)(need >> 32);
+        uint64_t mn = ~0ull;
+        for (uint64_t b = grp; b; b &= b - 1) {  // scalar walk over the window's bidders
+          const int l = __ffsll((unsigned long long)b) - 1;
+          const uint64_t v = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)nhi, l) << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane((int)nlo, l);
+          mn = v < mn ? v : mn;
+        }
+        if (lane == ld)
+          atomicMax(reinterpret_cast<unsigned long long *>(pa.bmin + (e_inv >> 6) + (int64_t)d * pa.nwin),
+                    (unsigned long long)(tag | (lo - (mn < lo ? mn : lo))));
+      }
+    }
+  }
   if (prop) {
     // bid tag: pass << 16 | parts << 8 | members (parts <= K <= 32, members <= 64)
     pa.bid[e_inv] = ((uint32_t)pass << 16) | ((uint32_t)np << 8) | (uint32_t)planned;
     pa.s0_out[e_inv] = s0;
-    // Long rows (k_csr_place, >= KP_BMIN_WIN windows): the window's smallest
-    // bid of this pass per dim — tighter than the round's smallest request,
-    // so accept skips, unread, the windows of a herded row none of whose
-    // bids of this pass fits (config #4's tail); the pass tag in the high
-    // bits makes atomicMax keep this pass's minimum. Short rows only flag
-    // the window (one plain store: atomics for every bid cost a config #3
-    // solve ~2.3 ms), which also tells accept the bid minima do not bound
-    // every bid of the window.
-    if (inv_raw < 0) {
-      const uint64_t tag = (uint64_t)(pass + 1) << 48, lo = (1ull << 48) - 1;
-      int64_t *bw = pa.bmin + (e_inv >> 6);
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        const uint64_t need = (uint64_t)planned * (uint64_t)qq[d];
-        atomicMax(reinterpret_cast<unsigned long long *>(bw + (int64_t)d * pa.nwin),
-                  (unsigned long long)(tag | (lo - (need < lo ? need : lo))));
-      }
-    } else {
-      pa.win[e_inv >> 6] = pass;
-    }
+    if (inv_raw >= 0) pa.win[e_inv >> 6] = pass;  // short row: the window flag
     pa.node_flag[node] = pass;
     if (np > 1) {
       const int idx = __popcll(pm & ((1ull << gl) - 1));

@@ -385,9 +385,7 @@ int launch_preempt(kp_ctx *c, int32_t *P_host, int32_t *lo, int32_t *hi) {
   hipLaunchKernelGGL(k_preempt_flags, dim3(blocks(U, 256)), dim3(256), 0, c->stream, c->d.status,
                      c->d.size, U, c->d.flag);
   KP_HIP(hipGetLastError());
-  size_t tb = c->d.temp_bytes;
-  KP_HIP(rocprim::select(c->d.temp, tb, rocprim::counting_iterator<int32_t>(0), c->d.flag,
-                         c->d.plist, c->d.counters, (size_t)U, c->stream));
+  KP_TRY(launch_compact_to(c, c->d.flag, 0, U, c->d.plist, nullptr));
   KP_HIP(hipMemcpyAsync(c->pinned, c->d.counters, sizeof(int32_t), hipMemcpyDeviceToHost,
                         c->stream));
   KP_HIP(hipStreamSynchronize(c->stream));

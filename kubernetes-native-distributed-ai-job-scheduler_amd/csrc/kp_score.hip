@@ -602,7 +602,16 @@ __global__ __launch_bounds__(256) void k_score32(ScoreParams sp,
 constexpr int kScoreClsRows = 64;  // rows per workgroup (LDS: rows x classes x record)
 constexpr int kClsCols = 4;        // columns per lane
 
-template <int D, bool MOST>
+// a kernel-argument (SGPR) value copied into a VGPR once: a select with a
+// compare mask in an SGPR pair may not read a second SGPR (one scalar operand
+// per VALU instruction on gfx950), so weights kept in SGPRs cost a v_mov per use
+__device__ __forceinline__ int32_t in_vgpr(int32_t s) {
+  int32_t v;
+  asm("v_mov_b32 %0, %1" : "=v"(v) : "s"(s));
+  return v;
+}
+
+template <int D, bool MOST, bool WS, bool WM>
 __global__ __launch_bounds__(256) void k_score32c(
     ScoreParams sp, const uint32_t *__restrict__ np, int32_t P, const int64_t *__restrict__ q,
     int32_t qstride, const int32_t *__restrict__ uaff, const int32_t *__restrict__ rows_unit,
@@ -613,10 +622,15 @@ __global__ __launch_bounds__(256) void k_score32c(
   constexpr int RW = (D + 1 + 3) & ~3;  // per (row, class): D thresholds + WQ, whole 16-B reads
   if (rows_dev) fit_rows(*rows_dev, min_rpb, rows, rows_per_block);
   if ((int)blockIdx.y * rows_per_block >= rows) return;  // block-uniform
+  // per row: the D requests, the GPU-dim request (0 if none) and the affinity domain
   __shared__ uint32_t sq[kScoreClsRows][D + 2];
   __shared__ __attribute__((aligned(16))) uint32_t sx[kScoreClsRows][kScoreClasses][RW];
   const int N = sp.N;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // wave index through readfirstlane: the compiler then knows that every
+  // per-wave quantity (tile0, the column groups, the row pointer) is uniform
+  // and branches on them with scalar branches (full EXEC: a ballot IS the
+  // fit mask, no re-materialisation)
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tile0 = blockIdx.x * (256 * NC) + wave * (64 * NC);  // this wave's first column
   const int r0 = blockIdx.y * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
@@ -628,14 +642,15 @@ __global__ __launch_bounds__(256) void k_score32c(
     uint32_t v;
     if (d == D + 1) {
       v = (uint32_t)uaff[unit];
+    } else if (d == D) {
+      v = g >= 0 ? (uint32_t)q[(int64_t)g * qstride + unit] : 0u;
     } else {
-      const int dd = d < D ? d : g;
-      v = dd >= 0 ? (uint32_t)q[(int64_t)dd * qstride + unit] : 0u;
+      v = (uint32_t)q[(int64_t)d * qstride + unit];
     }
     sq[rr][d] = v;
   }
   // the lane's columns tile0 + 64k + lane (P % 1024 == 0: inside the planes)
-  uint32_t f_[NC][D], a_[NC][D], fg_[NC], tp_[NC], cl_[NC];
+  uint32_t f_[NC][D], a_[NC][D], fg_[NC], tp_[NC], xo_[NC];
   int32_t b_[NC], wa_[NC];
   bool v_[NC];
 #pragma unroll
@@ -647,10 +662,11 @@ __global__ __launch_bounds__(256) void k_score32c(
       f_[k][d] = np[(int64_t)(kPlanes * d + 0) * P + col];
       a_[k][d] = np[(int64_t)(kPlanes * d + 2) * P + col];
     }
-    b_[k] = (int32_t)np[(int64_t)(kPlanes * D) * P + col];
+    b_[k] = MOST ? 0 : (int32_t)np[(int64_t)(kPlanes * D) * P + col];
     tp_[k] = np[(int64_t)(kPlanes * D + 1) * P + col];
     wa_[k] = (int32_t)np[(int64_t)(kPlanes * D + 2) * P + col];
-    cl_[k] = min(np[(int64_t)(kPlanes * D + 3) * P + col], (uint32_t)(kScoreClasses - 1));
+    // byte offset of the column's class record in a row of sx
+    xo_[k] = min(np[(int64_t)(kPlanes * D + 3) * P + col], (uint32_t)(kScoreClasses - 1)) * (RW * 4);
     fg_[k] = 0xFFFFFFFFu;  // free GPUs: never equal to a request when there is no GPU dim
 #pragma unroll
     for (int d = 0; d < D; ++d)
@@ -663,16 +679,13 @@ __global__ __launch_bounds__(256) void k_score32c(
     for (int t = threadIdx.x; t < ncl * nr; t += blockDim.x) {
       const int k = t / nr, rr = t - k * nr;
       uint32_t wq = 0;
-      bool ok = true;
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         const uint32_t c = ccap[k * D + d], qd = sq[rr][d];
-        uint32_t thr = 0xFFFFFFFFu;  // cap-0 dim: contributes 0, fits only q = 0
-        if (c == 0u) {
-          ok &= qd == 0u;
-        } else if (qd > c) {
-          ok = false;
-        } else {
+        // cap-0 dim: contributes 0 (fits only q = 0); q > c: fits no node of
+        // the class — both rejected by the per-node fit test q <= free <= c
+        uint32_t thr = 0xFFFFFFFFu;
+        if (c != 0u && qd <= c) {
           uint64_t Q, rho;
           udivmod_uniform((uint64_t)qd * S, c, Q, rho);
           thr = c - (uint32_t)rho;  // in (0, c]: carry iff a >= thr
@@ -680,50 +693,71 @@ __global__ __launch_bounds__(256) void k_score32c(
         }
         sx[rr][k][d] = thr;
       }
-      sx[rr][k][D] = ok ? wq : kRowNoFit;
+      sx[rr][k][D] = wq;
     }
   }
   __syncthreads();
   if (tile0 >= Ns) return;  // wave-uniform, after the last barrier
-  const int32_t wfit = sp.w_gpu_fit, waff = sp.w_affinity;
+  const int nk = min(NC, (Ns - tile0) >> 6);  // column groups inside the row stride
+  int32_t w_[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) w_[d] = in_vgpr(sp.w[d]);
+  const int32_t wfit = in_vgpr(sp.w_gpu_fit), waff = in_vgpr(sp.w_affinity);
+  const char *sxb = reinterpret_cast<const char *>(&sx[0][0][0]);
   for (int r = r0; r < r1; ++r) {
+    const int rr = r - r0;
+    // the row's requests are wave-uniform: scalar operands of the compares
     uint32_t qq[D];
 #pragma unroll
-    for (int d = 0; d < D; ++d) qq[d] = sq[r - r0][d];
-    const uint32_t qg = sq[r - r0][D], af = sq[r - r0][D + 1];
-    int32_t *srow = score ? score + (int64_t)r * sstride + tile0 + lane : nullptr;
+    for (int d = 0; d < D; ++d) qq[d] = __builtin_amdgcn_readfirstlane(sq[rr][d]);
+    const uint32_t qg = __builtin_amdgcn_readfirstlane(sq[rr][D]);
+    const uint32_t af = __builtin_amdgcn_readfirstlane(sq[rr][D + 1]);
+    const int32_t wfit_r = qg != 0u ? wfit : 0;  // the bonus needs a GPU request
+    // every class record of the row's columns first (LDS broadcasts: the lanes
+    // of one class read one address), then the arithmetic
+    uint32_t x[NC][RW];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const uint4 *rec = reinterpret_cast<const uint4 *>(sxb + rr * (kScoreClasses * RW * 4) + xo_[k]);
+#pragma unroll
+      for (int i = 0; i < RW / 4; ++i) {
+        const uint4 t4 = rec[i];
+        x[k][4 * i] = t4.x;
+        x[k][4 * i + 1] = t4.y;
+        x[k][4 * i + 2] = t4.z;
+        x[k][4 * i + 3] = t4.w;
+      }
+    }
+    int32_t *srow = WS ? score + (int64_t)r * sstride + tile0 : nullptr;  // wave-uniform
     uint64_t word[NC];
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
-      uint32_t x[RW];
-#pragma unroll
-      for (int i = 0; i < RW / 4; ++i) {
-        const uint4 t4 = reinterpret_cast<const uint4 *>(sx[r - r0][cl_[k]])[i];
-        x[4 * i] = t4.x;
-        x[4 * i + 1] = t4.y;
-        x[4 * i + 2] = t4.z;
-        x[4 * i + 3] = t4.w;
-      }
-      bool ft = v_[k] && !(x[D] & kRowNoFit);
-      int32_t acc = wa_[k] + (int32_t)(x[D] & ~kRowNoFit);
+      bool ft = v_[k];
+      int32_t acc = wa_[k] + (int32_t)x[k][D];
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         ft &= qq[d] <= f_[k][d];
-        acc += a_[k][d] >= x[d] ? sp.w[d] : 0;
+        acc += a_[k][d] >= x[k][d] ? w_[d] : 0;
       }
-      const int32_t bonus = ((qg != 0u && fg_[k] == qg) ? wfit : 0) + (tp_[k] == af ? waff : 0);
+      // GPU-topology fit (the job takes exactly the node's free GPUs) and the
+      // CacheStrategy=shared affinity domain
+      const int32_t bonus = (fg_[k] == qg ? wfit_r : 0) + (tp_[k] == af ? waff : 0);
       const int32_t sc = (MOST ? acc : b_[k] - acc) + bonus;
-      // the matrix is streamed out once: non-temporal stores (1.10-1.14 -> 1.01-1.04 ms
-      // per config #3 call; the mask's 32-B pieces stay cached, non-temporal: +0.06 ms)
-      if (srow && tile0 + 64 * k < Ns)
-        __builtin_nontemporal_store(ft ? sc : KP_SCORE_INFEASIBLE, srow + 64 * k);
+      // the ballot in the block of the compares (across the store's branch
+      // the compiler re-materialises the mask through a VGPR)
       word[k] = __ballot(ft);  // columns tile0 + 64k .. + 63: mask word (tile0 >> 6) + k
+      // the matrix is streamed out once: non-temporal stores (1.10-1.14 ->
+      // 1.01-1.04 ms per config #3 call; the mask's 32-B pieces stay cached)
+      if (WS && k < nk) __builtin_nontemporal_store(ft ? sc : KP_SCORE_INFEASIBLE, srow + 64 * k + lane);
     }
-    if (mask && lane < NC && tile0 + 64 * lane < Ns) {
-      uint64_t wd = word[0];
+    if (WM) {  // lane k < nk stores word k (scalar values written into lanes)
+      uint32_t lo = 0u, hi = 0u;
 #pragma unroll
-      for (int k = 1; k < NC; ++k) wd = lane == k ? word[k] : wd;
-      mask[(int64_t)r * mstride + (tile0 >> 6) + lane] = wd;
+      for (int k = 0; k < NC; ++k) {
+        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(lo) : "s"((uint32_t)word[k]), "n"(k));
+        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(hi) : "s"((uint32_t)(word[k] >> 32)), "n"(k));
+      }
+      if (lane < nk) mask[(int64_t)r * mstride + (tile0 >> 6) + lane] = ((uint64_t)hi << 32) | lo;
     }
   }
 }
@@ -1097,18 +1131,31 @@ __global__ void k_delta_check(int32_t K, int32_t N, int32_t D, const int32_t *__
 constexpr int kCompactBS = 1024, kCompactIPT = 16;
 // FROM_STATUS: the flags are status[lo + i] == kActive, read straight from the
 // unit status (k_round_begin); else the flag array of k_round_start
+// The multi-workgroup form (k_compact_count + k_compact_multi: one chunk per
+// workgroup, each starting at the sum of the earlier chunks' counts) covers
+// any n in two launches; it replaced rocprim::select (lookback init +
+// partition) in the compactions above the one-workgroup range and in
+// kp_preempt's preemptor list.
+constexpr int kCompactChunk = kCompactBS * kCompactIPT;
+// FROM_STATUS: the flags are status[lo + i] == kActive, read straight from the
+// unit status (k_round_begin); else the flag array of k_round_start.
+// Chunks [base_begin, base_end) of the flags, output from position carry0; the
+// count (carry0 + the range's flags) is stored when `count` is given.
 template <bool FROM_STATUS>
 __device__ __forceinline__ void compact_wg(const int32_t *__restrict__ flag, int32_t n,
                                            int32_t lo, int32_t *__restrict__ out,
                                            int32_t *__restrict__ count,
-                                           int32_t *__restrict__ host_count) {
+                                           int32_t *__restrict__ host_count,
+                                           int32_t base_begin = 0, int32_t base_end = INT32_MAX,
+                                           int32_t carry0 = 0) {
   __shared__ int32_t wsum[kCompactBS / kWave];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   // 16-B loads need a 16-B aligned start (status + lo: lo % 4 == 0)
   const bool vec = !FROM_STATUS || (lo & 3) == 0;
   const int32_t *src = FROM_STATUS ? flag + lo : flag;
-  int32_t carry = 0;
-  for (int32_t base = 0; base < n; base += kCompactBS * kCompactIPT) {
+  int32_t carry = carry0;
+  const int32_t bend = min(n, base_end);
+  for (int32_t base = base_begin; base < bend; base += kCompactChunk) {
     const int32_t i0 = base + t * kCompactIPT;
     int32_t f[kCompactIPT];
     if (vec && i0 + kCompactIPT <= n) {  // 16-B aligned (device allocation), i0 % 16 == 0
@@ -1152,7 +1199,7 @@ __device__ __forceinline__ void compact_wg(const int32_t *__restrict__ flag, int
     carry += total;
     __syncthreads();  // wsum reused by the next chunk
   }
-  if (t == 0) {
+  if (t == 0 && count) {
     *count = carry;
     // the host's copy (pinned, coherent): a system-scope vector store, no
     // copy command and no event in the stream
@@ -1165,6 +1212,53 @@ __global__ __launch_bounds__(kCompactBS) void k_compact(const int32_t *__restric
                                                         int32_t *__restrict__ count,
                                                         int32_t *__restrict__ host_count) {
   compact_wg<false>(flag, n, lo, out, count, host_count);
+}
+
+// set flags of chunk blockIdx.x -> bcount[blockIdx.x]
+__global__ __launch_bounds__(kCompactBS) void k_compact_count(const int32_t *__restrict__ flag,
+                                                              int32_t n,
+                                                              int32_t *__restrict__ bcount) {
+  __shared__ int32_t wsum[kCompactBS / kWave];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t i0 = (int64_t)blockIdx.x * kCompactChunk + (int64_t)t * kCompactIPT;
+  int32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < kCompactIPT; ++k) c += i0 + k < n && flag[i0 + k] != 0 ? 1 : 0;
+#pragma unroll
+  for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
+  if (lane == 0) wsum[w] = c;
+  __syncthreads();
+  if (t == 0) {
+    int32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kCompactBS / kWave; ++k) s += wsum[k];
+    bcount[blockIdx.x] = s;
+  }
+}
+
+// chunk blockIdx.x compacted at the sum of the earlier chunks' counts; the
+// last chunk stores the total count
+__global__ __launch_bounds__(kCompactBS) void k_compact_multi(const int32_t *__restrict__ flag,
+                                                              int32_t n, int32_t lo,
+                                                              const int32_t *__restrict__ bcount,
+                                                              int32_t *__restrict__ out,
+                                                              int32_t *__restrict__ count,
+                                                              int32_t *__restrict__ host_count) {
+  __shared__ int32_t psum[kCompactBS / kWave];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int32_t c = 0;
+  for (int32_t b = t; b < (int32_t)blockIdx.x; b += kCompactBS) c += bcount[b];
+#pragma unroll
+  for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_xor(c, d, kWave);
+  if (lane == 0) psum[w] = c;
+  __syncthreads();
+  int32_t carry0 = 0;
+#pragma unroll
+  for (int k = 0; k < kCompactBS / kWave; ++k) carry0 += psum[k];
+  const int32_t base = (int32_t)blockIdx.x * kCompactChunk;
+  const bool last = blockIdx.x + 1 == gridDim.x;
+  compact_wg<false>(flag, n, lo, out, last ? count : nullptr, last ? host_count : nullptr, base,
+                    base + kCompactChunk, carry0);
 }
 
 // Round start and compaction in ONE launch (one-workgroup compaction range):
@@ -1224,19 +1318,32 @@ struct ScoreL {
         const int rpb =
             (int)std::min<int64_t>(kScoreClsRows, std::max<int64_t>(c->score_min_rpb, want));
         const dim3 grid(ctiles, blocks(rows, rpb));
-#define KP_SC32C(M)                                                                           \
-  hipLaunchKernelGGL((k_score32c<D, M>), grid, dim3(256), 0, c->stream, sp, c->d.np32, P, q,      \
-                     qstride, c->d.aff, rows_unit, rows, rpb, c->score_min_rpb, score,            \
+#define KP_SC32C(M, WS_, WM_)                                                                  \
+  hipLaunchKernelGGL((k_score32c<D, M, WS_, WM_>), grid, dim3(256), 0, c->stream, sp, c->d.np32, P, \
+                     q, qstride, c->d.aff, rows_unit, rows, rpb, c->score_min_rpb, score,           \
                      sstride > 0 ? sstride : (int64_t)Ns, mask, mstride > 0 ? mstride : (int64_t)Ns / 64, \
                      Ns, rows_dev, c->d.ccap, c->n_classes)
-        if (sp.most_allocated)
-          KP_SC32C(true);
-        else
-          KP_SC32C(false);
+#define KP_SC32C_M(WS_, WM_)     \
+  if (sp.most_allocated)         \
+    KP_SC32C(true, WS_, WM_);    \
+  else                           \
+    KP_SC32C(false, WS_, WM_);
+        if (score && mask) {
+          KP_SC32C_M(true, true)
+        } else if (score) {
+          KP_SC32C_M(true, false)
+        } else if (mask) {
+          KP_SC32C_M(false, true)
+        }
+#undef KP_SC32C_M
 #undef KP_SC32C
         KP_HIP(hipGetLastError());
         return KP_OK;
       }
+      // only the class form takes caller row strides (k_score32 / k_score
+      // write rows of Ns scores and Ns / 64 mask words)
+      if ((sstride > 0 && sstride != Ns) || (mstride > 0 && mstride != Ns / 64))
+        { kp_set_error_msg("launch_score: row strides need the capacity-class form"); return KP_EINVAL; }
       const int64_t want = ((int64_t)rows * tiles + c->score_wg_target - 1) / c->score_wg_target;
       const int rpb =
           (int)std::min<int64_t>(kScoreMaxRows, std::max<int64_t>(c->score_min_rpb, want));
@@ -1252,6 +1359,8 @@ struct ScoreL {
       }
 #undef KP_SC32
     } else {
+      if ((sstride > 0 && sstride != Ns) || (mstride > 0 && mstride != Ns / 64))
+        { kp_set_error_msg("launch_score: row strides need the capacity-class form"); return KP_EINVAL; }
       constexpr int NPL = D <= 4 ? 2 : 1;
       const int rpb = 32;
       dim3 grid(blocks(Ns, 256 * NPL), blocks(rows, rpb));
@@ -1389,19 +1498,34 @@ static int launch_round_start(kp_ctx *c, int32_t lo, int32_t hi, int32_t *flag) 
 
 int launch_pack(kp_ctx *c) { return launch_round_start(c, 0, 0, nullptr); }
 
-// flags[0, n) -> act_local (lo + index, rank order), count -> counters[0]; one
-// workgroup up to KP_COMPACT_MAX flags (default 262,144), rocprim::select above
-static int launch_compact(kp_ctx *c, const int32_t *flag, int32_t lo, int32_t n, size_t tb,
-                          int32_t *host_count = nullptr) {
+// flags[0, n) -> out (lo + index, rank order; act_local by default), count ->
+// counters[0]; one workgroup up to KP_COMPACT_MAX flags (default 262,144),
+// the two-launch multi-workgroup form above (chunk counts in `temp`)
+int launch_compact_to(kp_ctx *c, const int32_t *flag, int32_t lo, int32_t n, int32_t *out,
+                      int32_t *host_count) {
   if (n <= c->compact_max) {
-    hipLaunchKernelGGL(k_compact, dim3(1), dim3(kCompactBS), 0, c->stream, flag, n, lo,
-                       c->d.act_local, c->d.counters, host_count);
+    hipLaunchKernelGGL(k_compact, dim3(1), dim3(kCompactBS), 0, c->stream, flag, n, lo, out,
+                       c->d.counters, host_count);
     KP_HIP(hipGetLastError());
     return KP_OK;
   }
-  KP_HIP(rocprim::select(c->d.temp, tb, rocprim::counting_iterator<int32_t>(lo), flag,
-                         c->d.act_local, c->d.counters, (size_t)n, c->stream));
+  const int chunks = blocks(n, kCompactChunk);
+  if ((size_t)chunks * sizeof(int32_t) > c->d.temp_bytes) {
+    kp_set_error_msg("launch_compact: chunk counts exceed the scratch buffer");
+    return KP_ENOMEM;
+  }
+  int32_t *bcount = reinterpret_cast<int32_t *>(c->d.temp);
+  hipLaunchKernelGGL(k_compact_count, dim3(chunks), dim3(kCompactBS), 0, c->stream, flag, n, bcount);
+  KP_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_compact_multi, dim3(chunks), dim3(kCompactBS), 0, c->stream, flag, n, lo,
+                     bcount, out, c->d.counters, host_count);
+  KP_HIP(hipGetLastError());
   return KP_OK;
+}
+
+static int launch_compact(kp_ctx *c, const int32_t *flag, int32_t lo, int32_t n, size_t /*tb*/,
+                          int32_t *host_count = nullptr) {
+  return launch_compact_to(c, flag, lo, n, c->d.act_local, host_count);
 }
 
 // active units of [lo, hi) in rank order -> act_local; count to host
@@ -1462,7 +1586,7 @@ int launch_active_async(kp_ctx *c, int32_t lo, int32_t hi, int32_t *count_host, 
   size_t tb = c->d.temp_bytes;
   // the one-workgroup compaction stores the count into coherent pinned
   // memory itself (count_direct); otherwise a copy lands it
-  const bool dir = direct && c->count_direct && c->pinned_coh && n <= c->compact_max;
+  const bool dir = direct && c->count_direct && c->pinned_coh;
   if (direct) *direct = dir;
   if (dir) {
     __atomic_store_n(c->pinned_coh, -1, __ATOMIC_RELAXED);  // the sentinel the host waits on

@@ -13,7 +13,8 @@
 //      chunk's rows (one exact division per (row, dim) lane), broadcasts them
 //      per row with v_readlane and writes its 128 scores of every row into a
 //      32-KB LDS tile;
-//   2. select — wave w reads row w of the chunk back (16 columns per lane):
+//   2. select — wave w reads row w of the chunk back (16 contiguous columns
+//      per lane, in a bank-rotated order):
 //      lane best of 32-bit truncated keys, bitonic sort of the 64 lane bests,
 //      T = the K-th of them (a lower bound of the tile's K-th key: K distinct
 //      columns reach it; truncation only keeps more), survivors >= T appended
@@ -419,12 +420,19 @@ void k_score_topk(
       // select-phase tie bits: (nst - tsp[g] - j * mt) >> rsh
       const uint32_t *tsp = tie0 ? spos0 : spos;
       const uint32_t nst = tie0 ? (spos[0] + 1023u) << 22 : nsl, mt = tie0 ? 1u << 22 : mul;
+      // lane L's 16 columns are the 4 groups 4L .. 4L + 3 (contiguous, so the
+      // survivor scan below reads one candidate lane's columns from 16
+      // consecutive LDS entries), visited in an order rotated by lane / 8
+      // (lane / 4 for 16-B groups): the lanes of one LDS access then cover
+      // every bank once (a plain 4L + k order would be 4-way conflicted)
+      constexpr int RSH = H16 ? 3 : 2;
       uint32_t best = 0;
 #pragma unroll 1
       for (int k = 0; k < 4; ++k) {
         uint32_t v4[4];
-        load_group<H16>(ssc[buf][i], lane + 64 * k, v4);
-        const uint32_t npk = nst - tsp[lane + 64 * k];
+        const int gk = 4 * lane + ((k + (lane >> RSH)) & 3);
+        load_group<H16>(ssc[buf][i], gk, v4);
+        const uint32_t npk = nst - tsp[gk];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const uint32_t s1 = v4[j];
@@ -463,7 +471,7 @@ void k_score_topk(
         uint32_t s1 = 0, ntk = 0;
         if (e < 16 * m) {
           const int L = scand[wave][e >> 4];          // candidate lane
-          const int g = L + 64 * ((e >> 2) & 3), jj = e & 3;  // its column group, column
+          const int g = 4 * L + ((e >> 2) & 3), jj = e & 3;  // its column group, column
           s1 = load_one<H16>(srow, 4 * g + jj);
           ntk = nsl - spos[g] - (uint32_t)jj * mul;
           hit = ((s1 << ksh) | ((nst - tsp[g] - (uint32_t)jj * mt) >> rsh)) >= T;
@@ -485,8 +493,8 @@ void k_score_topk(
 #pragma unroll 1
           for (int e = 0; e < 16; ++e) {
             const int k = e >> 2, j = e & 3;
-            const uint32_t s1 = load_one<H16>(srow, 4 * (lane + 64 * k) + j);
-            const uint32_t ntk = nsl - spos[lane + 64 * k] - (uint32_t)j * mul;
+            const uint32_t s1 = load_one<H16>(srow, 4 * (4 * lane + k) + j);
+            const uint32_t ntk = nsl - spos[4 * lane + k] - (uint32_t)j * mul;
             c += (s1 != 0u && (((uint64_t)(0x80000000u | (s1 - 1u)) << 32) | ntk) >= cb) ? 1 : 0;
           }
           c = (int)rl((uint32_t)wave_incl_scan_i32(c), 63);
@@ -496,8 +504,8 @@ void k_score_topk(
 #pragma unroll 1
         for (int e = 0; e < 16; ++e) {
           const int k = e >> 2, j = e & 3;
-          const uint32_t s1 = load_one<H16>(srow, 4 * (lane + 64 * k) + j);
-          const uint32_t ntk = nsl - spos[lane + 64 * k] - (uint32_t)j * mul;
+          const uint32_t s1 = load_one<H16>(srow, 4 * (4 * lane + k) + j);
+          const uint32_t ntk = nsl - spos[4 * lane + k] - (uint32_t)j * mul;
           const uint64_t key = ((uint64_t)(0x80000000u | (s1 - 1u)) << 32) | ntk;
           const bool hit = s1 != 0u && key >= pre;
           const uint64_t m = __ballot(hit);

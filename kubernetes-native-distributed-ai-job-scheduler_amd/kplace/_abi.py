@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-KP_ABI_VERSION = 6
+KP_ABI_VERSION = 7
 KP_MAX_DIMS = 8
 KP_MAX_CAND = 32
 KP_MAX_GANG = 64
@@ -96,6 +96,7 @@ class Timing(C.Structure):
         ("score_launches", C.c_int64), ("score_bytes", C.c_int64),
         ("select_bytes", C.c_int64), ("fused", C.c_int32), ("score_form", C.c_int32),
         ("score_classes", C.c_int32), ("pad", C.c_int32),
+        ("cand_ms", C.c_double), ("xchg_ms", C.c_double), ("pass_ms", C.c_double),
     ]
 
 

@@ -46,11 +46,12 @@ class DeviceBuffer:
         if fill is not None and h.hipMemset(self.ptr, fill, self.nbytes) != 0:
             raise RuntimeError("hipMemset failed")
 
-    def to_numpy(self, dtype, shape) -> np.ndarray:
+    def to_numpy(self, dtype, shape, offset: int = 0) -> np.ndarray:
+        """Bytes [offset, offset + size) of the buffer as an array."""
         out = np.empty(shape, dtype)
-        if out.nbytes > self.nbytes:
+        if offset < 0 or offset + out.nbytes > self.nbytes:
             raise ValueError("buffer smaller than the requested array")
-        if hip().hipMemcpy(out.ctypes.data, self.ptr, out.nbytes, 2) != 0:  # DeviceToHost
+        if hip().hipMemcpy(out.ctypes.data, self.ptr + offset, out.nbytes, 2) != 0:  # DeviceToHost
             raise RuntimeError("hipMemcpy failed")
         return out
 

@@ -215,8 +215,10 @@ class Placer:
         _check(lib().kp_score_dev(self._h, C.byref(params), lo, hi, C.c_void_p(score_ptr or None),
                                   C.c_void_p(mask_ptr or None)), "kp_score_dev", self._h)
 
-    def set_profiling(self, on: bool) -> None:
-        _check(lib().kp_set_profiling(self._h, 1 if on else 0), "kp_set_profiling", self._h)
+    def set_profiling(self, on) -> None:
+        """False/0 off, True/1 filter+score events, 2 also the per-round phase split."""
+        level = int(on) if not isinstance(on, bool) else (1 if on else 0)
+        _check(lib().kp_set_profiling(self._h, level), "kp_set_profiling", self._h)
 
     def timing(self) -> dict:
         t = _abi.Timing()

@@ -395,22 +395,28 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
   }
   st->pairs += (int64_t)active0 * N;
 
-  const char *trace_env = getenv("KPO_TRACE"); /* per-round counts on stderr (analysis) */
-  const int trace = trace_env ? (atoi(trace_env) > 2 ? 3 : atoi(trace_env) > 1 ? 2 : 1) : 0;
+  const char *trace_env = getenv("KPO_TRACE"); /* KPO_TRACE=1: per-round counts on stderr */
   int32_t passes0 = st->passes;
-  /* KPO_DUMP=path (analysis, tools/accept_sim.py): per round the candidates,
-     per pass the proposals with their first-fit outcome, appended as int32 */
+#ifdef KPO_ANALYSIS
+  /* analysis build only (make -C oracle analysis, tools/): KPO_TRACE=2/3
+     per-pass and accept-row statistics; KPO_DUMP=path (tools/accept_sim.py):
+     per round the candidates, per pass the proposals with their first-fit
+     outcome, appended as int32 */
+  const int trace = trace_env ? (atoi(trace_env) > 2 ? 3 : atoi(trace_env) > 1 ? 2 : 1) : 0;
   FILE *dump = getenv("KPO_DUMP") ? fopen(getenv("KPO_DUMP"), "ab") : NULL;
   if (dump) {
     int32_t h[4] = {-1, st->rounds, U, K};
     fwrite(h, sizeof h, 1, dump);
     fwrite(cand, sizeof(int32_t), (size_t)U * K, dump);
   }
-  int32_t *chg_pass = NULL; /* KPO_TRACE=2 analysis: last pass that changed each node's usage */
-  if (trace == 2) {
+  int32_t *chg_pass = NULL; /* last pass that changed each node's usage */
+  if (trace >= 2) {
     chg_pass = (int32_t *)malloc(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
     for (int32_t n = 0; chg_pass && n < N; ++n) chg_pass[n] = -2;
   }
+#else
+  const int trace = trace_env && atoi(trace_env) > 0 ? 1 : 0;
+#endif
   for (int pass = 0; pass < st->p.max_passes; ++pass) {
     /* proposals of every open unit, planned against the current usage */
     int32_t np = 0;
@@ -426,6 +432,7 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
     if (np == 0) break;
     st->passes++;
     qsort(props, np, sizeof *props, cmp_prop);
+#ifdef KPO_ANALYSIS
     if (trace > 1) { /* KPO_TRACE=2: per-pass open units, proposals, bid nodes */
       int32_t nopen = 0, nodes = 0, dirty = 0, nchg = 0;
       for (int32_t u = 0; u < U; ++u) nopen += open[u];
@@ -443,9 +450,12 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
       fprintf(stderr, "kpo pass %d.%d open %d props %d nodes %d changed %d dirty %d\n", st->rounds, pass,
               nopen, np, nodes, nchg, dirty);
     }
+#endif
     /* per node, in unit rank order: first-fit against the remaining capacity */
     int64_t rem[KP_MAX_DIMS];
-    int32_t tr_maxrow = 0, tr_maxlast = 0, tr_maxsuf = 0; /* KPO_TRACE=3 (analysis) */
+#ifdef KPO_ANALYSIS
+    int32_t tr_maxrow = 0, tr_maxlast = 0, tr_maxsuf = 0; /* KPO_TRACE=3 */
+#endif
     for (int32_t i = 0; i < np;) {
       int32_t node = props[i].node, e = i;
       while (e < np && props[e].node == node) ++e;
@@ -461,6 +471,7 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
         if (fits)
           for (int d = 0; d < D; ++d) rem[d] -= (int64_t)props[k].count * q[d];
       }
+#ifdef KPO_ANALYSIS
       if (trace > 2) {
         /* bids of the row; index of its last accepted bid; bids walked until the
            remaining capacity is below the smallest later request in some dim */
@@ -488,8 +499,10 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
         if (last + 1 > tr_maxlast) tr_maxlast = last + 1;
         if (suf > tr_maxsuf) tr_maxsuf = suf;
       }
+#endif
       i = e;
     }
+#ifdef KPO_ANALYSIS
     if (trace > 2)
       fprintf(stderr, "kpo accept %d.%d maxrow %d maxlast %d maxsuf %d\n", st->rounds, pass, tr_maxrow,
               tr_maxlast, tr_maxsuf);
@@ -501,6 +514,7 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
         fwrite(r, sizeof r, 1, dump);
       }
     }
+#endif
     /* all-or-nothing: a unit is placed iff every proposal was accepted */
     for (int32_t k = 0; k < np; ++k) gang_bad[props[k].unit] = 0;
     for (int32_t k = 0; k < np; ++k)
@@ -512,7 +526,9 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
       unit_req(st, u, q);
       for (int d = 0; d < D; ++d)
         st->used[(int64_t)d * N + props[k].node] += (int64_t)props[k].count * q[d];
+#ifdef KPO_ANALYSIS
       if (chg_pass) chg_pass[props[k].node] = pass;
+#endif
       for (int32_t m = 0; m < props[k].count; ++m) {
         st->job_node[st->leader[u] + props[k].member_off + m] = props[k].node;
         st->job_score[st->leader[u] + props[k].member_off + m] = props[k].score;
@@ -524,8 +540,10 @@ int32_t kpo_round_run(kpo_state *st, const int32_t *cand) {
   if (trace)
     fprintf(stderr, "kpo round %d active %d passes %d\n", st->rounds, active0, st->passes - passes0);
   st->rounds++;
+#ifdef KPO_ANALYSIS
   if (dump) fclose(dump);
   free(chg_pass);
+#endif
   free(open); free(props); free(ok); free(gang_bad);
   return kpo_state_active(st);
 }

@@ -5,11 +5,16 @@ oracle (test infrastructure), so that the GPU box only runs the GPU side:
   config4   200k pending x 20k nodes, 30% GPU occupancy of running jobs:
             placement + preemption nominations (kpo_preempt);
   config5   the first 3 micro-batches (5k jobs each) of the 1M-job trace
-            against the 50k-node table, with the 20% completions between them.
+            against the 50k-node table, with the 20% completions between them;
+  config3_score  the materialised filter + score outputs (kpo_score) of the
+            whole config #3 queue, 100k x 10k: the int32 score matrix (N
+            columns per row) and the feasibility bitmask (ceil(N/64) words per
+            row), row after row, as two SHA-256 digests.
 
 Each entry holds SHA-256 digests of the int arrays (little-endian bytes) plus
 the scalar counters; the inputs' digests pin the generator. Run from the repo
-root: python tests/golden/make_large.py  (minutes on 8 cores).
+root: python tests/golden/make_large.py [entry ...]  (minutes on 8 cores; named
+entries are recomputed, the others kept).
 """
 import hashlib
 import json
@@ -80,12 +85,36 @@ def config5_entry(threads, batches=3, total=1_000_000, N=50_000, B=5_000):
     return out
 
 
+def config3_score_entry(threads, chunk=4_000):
+    w = synth.config3()
+    p = _abi.default_params(**synth.CONFIG_PARAMS[3])
+    sb = ob.SnapshotBuf.from_workload(w)
+    hs, hm = hashlib.sha256(), hashlib.sha256()
+    feasible = 0
+    t = time.time()
+    for lo in range(0, w.J, chunk):
+        sc, mk = ob.score(sb, p, lo, min(w.J, lo + chunk))
+        hs.update(sc.astype("<i4").tobytes())
+        hm.update(mk.astype("<u8").tobytes())
+        feasible += int((sc >= 0).sum())
+    print(f"config3_score oracle {time.time() - t:.1f}s, {feasible} feasible pairs", flush=True)
+    return {"inputs": {"req": digest(w.req), "cap": digest(w.cap), "used": digest(w.used)},
+            "rows": w.J, "nodes": w.N, "score": hs.hexdigest(), "mask": hm.hexdigest(),
+            "feasible_pairs": feasible}
+
+
+ENTRIES = {"config5": config5_entry, "config4": config4_entry, "config3_score": config3_score_entry}
+
+
 def main():
     threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
     ob.build()
-    res = {"generator": "tests/golden/make_large.py", "config5": config5_entry(threads),
-           "config4": config4_entry(threads)}
-    with open(os.path.join(HERE, "large_digests.json"), "w") as f:
+    path = os.path.join(HERE, "large_digests.json")
+    res = json.load(open(path)) if os.path.exists(path) else {}
+    res["generator"] = "tests/golden/make_large.py"
+    for name in sys.argv[1:] or list(ENTRIES):
+        res[name] = ENTRIES[name](threads)
+    with open(path, "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
     print("wrote large_digests.json")
 

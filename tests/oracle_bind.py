@@ -20,7 +20,8 @@ if PKG not in sys.path:
 from kplace import _abi  # noqa: E402
 
 ORACLE_DIR = os.path.join(REPO, "oracle")
-ORACLE_SO = os.path.join(ORACLE_DIR, "libkp_oracle.so")
+# KPO_LIB: the analysis build (make -C oracle analysis) for tools/ scripts
+ORACLE_SO = os.environ.get("KPO_LIB") or os.path.join(ORACLE_DIR, "libkp_oracle.so")
 
 
 _lib = None

@@ -29,6 +29,48 @@ def digest(a) -> str:
     return hashlib.sha256(a.astype(a.dtype.newbyteorder("<")).tobytes()).hexdigest()
 
 
+def test_score_dev_full_size_config3():
+    """kp_score_dev over the WHOLE config #3 queue (100k x 10k, the bench's
+    score_matrix leg) into caller device buffers: the score matrix and the
+    feasibility bitmask equal the oracle's (kpo_score) SHA-256 digests; the
+    padding columns are infeasible; the score-only and mask-only kernel
+    instances write the same bytes."""
+    from kplace.devmem import DeviceBuffer
+    w = synth.config3()
+    g3 = GOLD["config3_score"]
+    assert {k: digest(v) for k, v in dict(req=w.req, cap=w.cap, used=w.used).items()} == g3["inputs"]
+    p = _abi.default_params(**synth.CONFIG_PARAMS[3])
+    J, N = w.J, w.N
+    Ns = (N + 63) // 64 * 64
+    words, uw = Ns // 64, (N + 63) // 64
+    chunk = 5_000
+    with DeviceBuffer(J * Ns * 4) as sc, DeviceBuffer(J * words * 8) as mk, \
+            DeviceBuffer(J * Ns * 4, fill=0) as sc2, DeviceBuffer(J * words * 8, fill=0) as mk2:
+        with Placer(device=0) as pl:
+            pl.load_nodes(w.cap, w.used, w.topo)
+            pl.load_jobs(w.req, w.prio, w.gang_id, w.gang_size)
+            pl.set_profiling(True)
+            pl.score_dev(p, 0, J, sc.ptr, mk.ptr)
+            t = pl.timing()
+            pl.score_dev(p, 0, J, sc2.ptr, None)
+            pl.score_dev(p, 0, J, None, mk2.ptr)
+        print(f"kp_score_dev full config #3: {t['score_ms']:.3f} ms, {t['score_launches']} launch(es)")
+        hs, hm = hashlib.sha256(), hashlib.sha256()
+        feasible = 0
+        for lo in range(0, J, chunk):
+            n = min(chunk, J - lo)
+            a = sc.to_numpy(np.int32, (n, Ns), offset=lo * Ns * 4)
+            assert (a[:, N:] == -1).all()
+            assert np.array_equal(a, sc2.to_numpy(np.int32, (n, Ns), offset=lo * Ns * 4))
+            m = mk.to_numpy(np.uint64, (n, words), offset=lo * words * 8)
+            assert np.array_equal(m, mk2.to_numpy(np.uint64, (n, words), offset=lo * words * 8))
+            hs.update(np.ascontiguousarray(a[:, :N]).astype("<i4").tobytes())
+            hm.update(np.ascontiguousarray(m[:, :uw]).astype("<u8").tobytes())
+            feasible += int((a[:, :N] >= 0).sum())
+    assert feasible == g3["feasible_pairs"]
+    assert hs.hexdigest() == g3["score"] and hm.hexdigest() == g3["mask"]
+
+
 def test_config4_full_size_parity_and_properties():
     w = synth.config4()
     m = w.meta

@@ -233,9 +233,9 @@ def test_score_geometry_parity(oracle, monkeypatch, knobs):
 
 @pytest.mark.parametrize("cmax", ["0", "3000"])
 def test_active_compaction_paths_parity(oracle, monkeypatch, cmax):
-    """The rocprim::select fallback of the active-unit compaction (every round,
-    or only the large early rounds) gives the same placement as the
-    one-workgroup kernel and the oracle."""
+    """The multi-workgroup form of the active-unit compaction (chunk counts +
+    chunk scatter; every round, or only the large early rounds) gives the
+    same placement as the one-workgroup kernel and the oracle."""
     monkeypatch.setenv("KP_COMPACT_MAX", cmax)
     w = synth.config3(20_000, 1_000)
     p = _abi.default_params(**synth.CONFIG_PARAMS[3])
@@ -243,6 +243,21 @@ def test_active_compaction_paths_parity(oracle, monkeypatch, cmax):
         g = pl.place(w, p)
     o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
     _assert_same(g, o, f"KP_COMPACT_MAX={cmax}")
+
+
+@pytest.mark.parametrize("cmax", ["0"])
+def test_preempt_compaction_paths_parity(oracle, monkeypatch, cmax):
+    """kp_preempt's preemptor list (and every round's active units) through
+    the multi-workgroup compaction (2 chunks of 16,384 flags) equals the
+    oracle's nominations (config #4's shape, 1/10 size)."""
+    monkeypatch.setenv("KP_COMPACT_MAX", cmax)
+    w = synth.config4(20_000, 2_000)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[4])
+    m = w.meta
+    with Placer(device=0) as pl:
+        g, gp, o, op = _preempt_both(oracle, pl, w, p, m["run_node"], m["run_req"], m["run_prio"])
+    _assert_same(g, o, f"config4 KP_COMPACT_MAX={cmax}")
+    _assert_same_pre(gp, op, f"config4 KP_COMPACT_MAX={cmax}")
 
 
 @pytest.mark.parametrize("knobs", [
@@ -1090,12 +1105,15 @@ def test_score_matrix_class_form(oracle, monkeypatch, classes, mode, scale, wide
         assert np.array_equal(mk, omk), f"classes {classes} knob {knob}"
 
 
-@pytest.mark.parametrize("cfg", [(2, 3_000, 1_000), (3, 4_000, 1_500), (4, 3_000, 2_000)])
-def test_score_dev_parity(oracle, cfg):
-    """kp_score_dev into torch-owned device buffers (padded rows of
-    round_up(N, 64)): the first N columns equal the oracle's matrix and mask,
-    padding columns are infeasible / zero bits; profiling reports the class
-    form and algorithmic bytes."""
+@pytest.mark.parametrize("cfg", [(2, 3_000, 1_000), (3, 4_000, 1_500), (4, 3_000, 2_000),
+                                 (3, 2_000, 3_001)])
+@pytest.mark.parametrize("outputs", ["both", "score", "mask"])
+def test_score_dev_parity(oracle, cfg, outputs):
+    """kp_score_dev into caller device buffers (padded rows of round_up(N, 64)):
+    the first N columns equal the oracle's matrix and mask, padding columns are
+    infeasible / zero bits; either output alone (the kernel's score-only and
+    mask-only instances) writes the same values and leaves the other buffer
+    untouched; profiling reports the class form and algorithmic bytes."""
     from kplace.devmem import DeviceBuffer
     no, J, N = cfg
     w = synth.config(no, J, N)
@@ -1108,12 +1126,20 @@ def test_score_dev_parity(oracle, cfg):
             pl.load_nodes(w.cap, w.used, w.topo)
             pl.load_jobs(w.req, w.prio, w.gang_id, w.gang_size)
             pl.set_profiling(True)
-            pl.score_dev(p, lo, hi, sc.ptr, mk.ptr)
+            pl.score_dev(p, lo, hi, sc.ptr if outputs != "mask" else None,
+                         mk.ptr if outputs != "score" else None)
             t = pl.timing()
         g = sc.to_numpy(np.int32, (hi - lo, Ns))
         gm = mk.to_numpy(np.uint64, (hi - lo, Ns // 64))
     osc, omk = oracle.score(_snap(oracle, w), p, lo, hi)
-    assert np.array_equal(g[:, :N], osc) and (g[:, N:] == -1).all()
-    assert np.array_equal(gm[:, :omk.shape[1]], omk)
-    assert t["score_form"] == 1 and t["score_classes"] >= 1 and t["score_bytes"] > (hi - lo) * Ns * 4
+    if outputs == "mask":
+        assert (g.view(np.uint32) == 0x5A5A5A5A).all()
+    else:
+        assert np.array_equal(g[:, :N], osc) and (g[:, N:] == -1).all()
+    if outputs == "score":
+        assert (gm == 0x5A5A5A5A5A5A5A5A).all()
+    else:
+        assert np.array_equal(gm[:, :omk.shape[1]], omk)
+    assert t["score_form"] == 1 and t["score_classes"] >= 1 and t["score_launches"] == 1
+    assert t["score_bytes"] > (hi - lo) * (Ns * 4 if outputs != "mask" else Ns // 8)
     assert t["score_ms"] > 0

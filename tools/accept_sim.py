@@ -7,7 +7,8 @@ usage, the window flags + minima of each 64-window chunk, and one level per
 batch of flagged windows that pass the window-minimum test. The per-pass
 critical path is the node with the most levels.
 
-  KPO_DUMP=/tmp/c3.dump python tools/round_shape.py 3 > /dev/null
+  make -C oracle analysis
+  KPO_LIB=$PWD/oracle/libkp_oracle_analysis.so KPO_DUMP=/tmp/c3.dump python tools/round_shape.py 3 > /dev/null
   python tools/accept_sim.py /tmp/c3.dump 3
   TAIL=1 ...: per pass, the node with the most decided windows (the tail of the
   launch): its bidder entries, windows, flagged windows, windows that pass the
