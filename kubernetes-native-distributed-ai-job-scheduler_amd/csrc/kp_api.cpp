@@ -452,7 +452,7 @@ static int load_nodes_impl(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap,
       fz_cols = ((fz_cols + 127) & ~(int64_t)127) + (e - i);
       i = e;
     }
-    const int64_t P = (std::max<int64_t>(fz_cols, 1) + 1023) & ~(int64_t)1023;
+    const int64_t P = (std::max<int64_t>(fz_cols, 1) + kFzTileMax - 1) & ~(int64_t)(kFzTileMax - 1);
     if (N > 0 && P <= ((int64_t)1 << 24)) {
       colnode.assign((size_t)P, -1);
       wshift.assign((size_t)(P / 128), 0);
@@ -823,14 +823,14 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   }
   const bool fused = c->fused_enabled && c->fz_layout_ok && c->fits32 &&
                      c->max_cap < ((int64_t)1 << 30) && c->max_req < ((int64_t)1 << 30) &&
-                     ksh >= 8 && (int64_t)(c->fz_P / 1024) * K <= 2048;
+                     ksh >= 8 && (int64_t)(c->fz_P / fz_tile(c)) * K <= 2048;
   c->pack_fused = fused;
   c->pack_full = true;
   c->last_fused = fused;
   int64_t rpc = rows_per_chunk(c);
   if (fused) {
     rpc = INT64_MAX;  // no matrix, no chunks: per row only tiles x K keys
-    KP_TRY(ensure_part(c, (int64_t)std::max(shard, 1) * (c->fz_P / 1024) * K));
+    KP_TRY(ensure_part(c, (int64_t)std::max(shard, 1) * (c->fz_P / fz_tile(c)) * K));
     if (!c->d.part || !c->d.colnode || !c->d.wshift)
       return fail(KP_ENOMEM, "kp_solve: a fused-path buffer is missing");
   } else {
@@ -1143,7 +1143,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     if (ke.round < (int32_t)round_active.size())
       rows = std::min<int64_t>(rows, round_active[ke.round]);
     if (fused) {  // compulsory bytes: requests in, per-tile lists out, node planes once
-      const int64_t lists = (int64_t)(c->fz_P / 1024) * K * 8;
+      const int64_t lists = (int64_t)(c->fz_P / fz_tile(c)) * K * 8;
       tm.score_bytes += rows * ((int64_t)8 * c->D + 12 + lists) +
                         (int64_t)(2 * c->D + 3) * 4 * c->fz_P;
       tm.select_bytes += rows * (lists + K * 4);  // k_merge_tour

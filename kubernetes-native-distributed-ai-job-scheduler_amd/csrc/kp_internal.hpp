@@ -31,6 +31,10 @@ enum UnitStatus : int32_t { kActive = 0, kPlaced = 1, kNoFit = 2 };
 // k_score32's class form (kp_score.hip): node tables with at most this many
 // distinct capacity vectors get per-(row, class) thresholds staged in LDS
 constexpr int kScoreClasses = 8;
+// k_score_topk workgroup: kFzWaves waves x 128 columns; the fused
+// candidate phase's layout is padded to whole tiles
+constexpr int kFzWaves = 8;
+constexpr int kFzTileMax = 128 * kFzWaves;
 
 // d.pass_flag layout: [0, 64) productive-pass flags of the current round
 constexpr int kPassFlagWords = 128;
@@ -399,3 +403,8 @@ void kp_set_error_msg(const std::string &msg);
     int rc_ = (expr);             \
     if (rc_ != KP_OK) return rc_; \
   } while (0)
+
+namespace kp {
+// columns of one k_score_topk workgroup tile (one per-row top-K list each)
+inline int fz_tile(const kp_ctx *) { return kFzTileMax; }
+}  // namespace kp

@@ -415,6 +415,28 @@ __global__ void k_csr_place(int32_t A, int32_t K, int32_t D, int32_t U, int64_t 
 // subtracts the spread penalty of its topo domain, and the group takes the
 // (max value, lowest lane). All first-level loads (slot state, unit, candidate,
 // entry index) are issued together, before the open test.
+// a wave-uniform (kernel-argument) value held in a VGPR: a compare-select
+// with its mask in an SGPR pair may read no second scalar operand
+__device__ __forceinline__ int32_t in_vgpr(int32_t x) {
+  int32_t r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
+  return r;
+}
+
+// floor(x / y) for y > 0, capped at 64: a float estimate (relative error
+// ~2^-21, so at most one off below the cap) corrected once each way with
+// exact 64-bit products
+__device__ __forceinline__ uint32_t floor_div_cap64(uint32_t x, uint32_t y) {
+  const float f = (float)x * __builtin_amdgcn_rcpf((float)y);
+  uint32_t c = f >= 64.f ? 64u : (uint32_t)f;
+  const uint64_t cy = (uint64_t)c * y;
+  if (cy > (uint64_t)x)
+    --c;
+  else if (c < 64u && cy + y <= (uint64_t)x)
+    ++c;
+  return c;
+}
+
 struct PlanArgs {
   ScoreParams sp;
   int32_t A;
@@ -549,54 +571,74 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
       acc_t += sp.w[d] * (int32_t)t_[d];
       wq[d] = sp.w[d] * (int32_t)Q_[d];
     }
-    // score of one more member on this lane's candidate (-1: it does not fit);
-    // changes only when this lane wins a member
-    auto cur_score = [&]() -> int32_t {
-      bool fits = valid;
-      int32_t acc = acc_t, bonus = abonus;
+    // Once per lane instead of per member: the (p+1)-th member fits this
+    // lane's candidate iff (p + 1)·q ≤ free in every dim, i.e. p < cnt =
+    // min_d ⌊free_d / q_d⌋ (capped at 64 ≥ any gang), and the GPU-fit bonus
+    // (the member takes exactly the node's last free GPUs) applies at the one
+    // p with (p + 1)·q_g = free_g. The member loop then only steps the
+    // utilisations of the winning lane.
+    uint32_t cnt = valid ? 64u : 0u;
+    int32_t pfit = -1;
 #pragma unroll
-      for (int d = 0; d < D; ++d) {
-        fits &= q32[d] <= rem[d];
-        if (!sp.most_allocated && r_[d] != 0) acc += sp.w[d];  // LeastAllocated: ceiling
-        if (d == g && q32[d] > 0 && rem[d] == q32[d]) bonus += sp.w_gpu_fit;
+    for (int d = 0; d < D; ++d) {
+      if (q32[d] != 0u) {
+        const uint32_t c = floor_div_cap64(rem[d], q32[d]);
+        cnt = min(cnt, c);
+        if (d == g && (uint64_t)c * q32[d] == rem[d]) pfit = (int32_t)c - 1;
       }
-      return fits ? (sp.most_allocated ? acc : b - acc) + bonus : -1;
-    };
-    int32_t sc = cur_score();
-    s0 = slot_ok ? sc : -1;  // the first member's score at pass-start usage
-    // the group's lanes in this lane's topo domain (the spread penalty counts
-    // members planned into the domain of the winning candidate)
-    uint32_t smask = 0;
+    }
+    // the group's lanes in this lane's topo domain, bit G-1-j for lane j (the
+    // spread penalty counts members planned into the domain of the winning
+    // candidate; a lane without a valid candidate counts none)
+    uint32_t rmask = 0;
 #pragma unroll
-    for (int j = 0; j < G; ++j) smask |= (__shfl(tp, gbase + j, kWave) == tp ? 1u : 0u) << j;
+    for (int j = 0; j < G; ++j) rmask |= (__shfl(tp, gbase + j, kWave) == tp ? 1u : 0u) << (G - 1 - j);
+    if (!valid) rmask = 0;
     KP_PP_MARK(1);
     // One 32-bit key per lane, (value + off) << log2 G | (G-1-lane): one group
     // max gives the best value and, among equal values, the lowest lane; key
     // 0 = infeasible. The host keeps value + off < 2^(32 - log2 G) and off =
     // 64·w_spread + 1 > any penalty (PlanArgs::key_off).
     constexpr int LB = G == 16 ? 4 : G == 32 ? 5 : 6;
+    const uint32_t lanebits = (uint32_t)(G - 1 - gl);
+    const bool most = sp.most_allocated;
+    int32_t wv[D];  // the weights in VGPRs (a select reads one scalar operand: its mask)
+#pragma unroll
+    for (int d = 0; d < D; ++d) wv[d] = in_vgpr(sp.w[d]);
+    const int32_t wfitv = in_vgpr(sp.w_gpu_fit), wspv = in_vgpr(sp.w_spread);
+    // score of one more member on this lane's candidate after p of its own
+    // (-1: it does not fit); changes only when this lane wins a member
+    auto score_at = [&](int32_t p) -> int32_t {
+      int32_t acc = acc_t;
+      if (!most) {  // LeastAllocated: the ceiling of every dim (wave-uniform branch)
+#pragma unroll
+        for (int d = 0; d < D; ++d) acc += r_[d] != 0u ? wv[d] : 0;
+      }
+      const int32_t bonus = abonus + (p == pfit ? wfitv : 0);
+      return (uint32_t)p < cnt ? (most ? acc : b - acc) + bonus : -1;
+    };
+    int32_t sc = score_at(0);
+    s0 = slot_ok ? sc : -1;  // the first member's score at pass-start usage
     int32_t pen = 0;  // w_spread x members planned into this lane's domain
     for (int m = 0; m < szmax; ++m) {
       const bool live = !fail && m < sz;  // group-uniform
-      const uint32_t key = (live && sc >= 0)
-                               ? ((uint32_t)(sc - pen + pa.key_off) << LB) | (uint32_t)(G - 1 - gl)
-                               : 0u;
+      const uint32_t key =
+          (live && sc >= 0) ? ((uint32_t)(sc - pen + pa.key_off) << LB) | lanebits : 0u;
       const uint32_t best = group_max_u32<G>(key);
       if (live && best == 0) fail = true;
       if (live && !fail) {
-        const int w = G - 1 - (int)(best & (G - 1));
-        if (gl == w) {
+        const uint32_t wb = best & (G - 1);  // G-1-(winning lane)
+        if (wb == lanebits) {
           ++planned;
 #pragma unroll
           for (int d = 0; d < D; ++d) {
-            rem[d] -= q32[d];
             const bool wrap = r_[d] >= thr[d];
             r_[d] = wrap ? r_[d] - thr[d] : r_[d] + rho[d];
-            acc_t += wq[d] + (wrap ? sp.w[d] : 0);
+            acc_t += wq[d] + (wrap ? wv[d] : 0);
           }
-          sc = cur_score();
+          sc = score_at(planned);
         }
-        pen += (valid && ((smask >> w) & 1u)) ? sp.w_spread : 0;
+        pen += (int32_t)((rmask >> wb) & 1u) * wspv;
       }
     }
   } else {
@@ -857,7 +899,15 @@ __device__ __forceinline__ void decide_window(const Win<D, N32> &wc,
     for (int d = 0; d < D; ++d) fa &= wc.need[d] <= rem[d];
     // lanes that do not fit alone are rejected for good; if none fits, the
     // window is done without any prefix scan
-    if (__ballot(fa) == 0) break;
+    const uint64_t fam = __ballot(fa);
+    if (fam == 0) break;
+    if ((fam & (fam - 1)) == 0) {  // one lane fits alone: it is accepted, no scans
+      const int l1 = __ffsll((unsigned long long)fam) - 1;
+      accepted |= fa;
+#pragma unroll
+      for (int d = 0; d < D; ++d) rem[d] -= readlane_nt(wc.need[d], l1);
+      break;
+    }
     bool okp = fa;
     NT pre[D];
 #pragma unroll

@@ -13,8 +13,8 @@
 //      chunk's rows (one exact division per (row, dim) lane), broadcasts them
 //      per row with v_readlane and writes its 128 scores of every row into a
 //      32-KB LDS tile;
-//   2. select — wave w reads row w of the chunk back (16 contiguous columns
-//      per lane, in a bank-rotated order):
+//   2. select — wave w reads row w of the chunk back (16 columns per lane,
+//      strided over the tile; rows padded so that no LDS access conflicts):
 //      lane best of 32-bit truncated keys, bitonic sort of the 64 lane bests,
 //      T = the K-th of them (a lower bound of the tile's K-th key: K distinct
 //      columns reach it; truncation only keeps more), survivors >= T appended
@@ -71,12 +71,21 @@ using namespace dev;
 #define KP_MERGE_WPB 4  // k_merge_tour rows (waves) per workgroup
 #endif
 constexpr int kMergeWPB = KP_MERGE_WPB;
-constexpr int kFzWaves = 8;
-constexpr int kFzBS = 64 * kFzWaves;
-constexpr int kFzTile = 128 * kFzWaves;  // columns per workgroup (2 per lane)
-constexpr int kFzRC = 8;                 // rows per LDS chunk: one per wave in the select
 constexpr int kFzMaxRows = 128;          // rows per workgroup (request stage)
 constexpr int kFzSurv = 128;             // survivor slots per wave (2 per lane)
+// Workgroup shape of k_score_topk: NW waves x 128 columns (2 per lane) =
+// the tile whose exact top-K one select per row produces. NW = 8: 1,024
+// columns, 3 workgroups per CU. (NW = 16 — 2,048 columns, one workgroup per
+// CU, half the per-(row, tile) select and merge work — measured slower in
+// r05: config #3 +0.2-1.5 ms, config #4 620 vs 552 ms)
+template <int NW>
+struct FzShape {
+  static constexpr int BS = 64 * NW;     // threads
+  static constexpr int TILE = 128 * NW;  // columns per workgroup
+  static constexpr int RC = NW;          // rows per LDS chunk: one per wave in the select
+  static constexpr int GPL = NW / 2;     // 4-column groups per lane in the select
+  static_assert(kFzTileMax % TILE == 0, "the tile width divides the layout's alignment");
+};
 
 template <int D>
 constexpr int fz_dp() {
@@ -152,34 +161,45 @@ __device__ __forceinline__ uint32_t load_one(const uint32_t *row, int col) {
 
 
 #ifndef KP_FZ_WAVES_PER_EU
-#define KP_FZ_WAVES_PER_EU 6  // 80 VGPRs: 3 workgroups of 8 waves per CU (a small spill is cheaper than 2)
+#define KP_FZ_WAVES_PER_EU 6  // NW = 8: 80 VGPRs, 3 workgroups of 8 waves per CU (a small spill is cheaper than 2)
 #endif
-template <int D, bool MOST, bool H16>
-__global__ __launch_bounds__(kFzBS)
-#if KP_FZ_WAVES_PER_EU
-__attribute__((amdgpu_waves_per_eu(KP_FZ_WAVES_PER_EU, KP_FZ_WAVES_PER_EU)))
-#endif
+template <int D, bool MOST, bool H16, int NW>
+__global__ __launch_bounds__(64 * NW)
+__attribute__((amdgpu_waves_per_eu(NW == 8 ? KP_FZ_WAVES_PER_EU : 4, NW == 8 ? KP_FZ_WAVES_PER_EU : 4)))
 void k_score_topk(
     ScoreParams sp, const uint32_t *__restrict__ np, int32_t P, const int64_t *__restrict__ q,
     int32_t qstride, const int32_t *__restrict__ uaff, const uint32_t *__restrict__ salt,
     const int32_t *__restrict__ rows_unit, int32_t rows, int32_t rows_per_block, int32_t min_rpb,
     const int32_t *__restrict__ rows_dev, const int32_t *__restrict__ wshift, int32_t ksh, int32_t tbits,
     uint64_t *__restrict__ part, uint64_t *__restrict__ prof) {
+  using FS = FzShape<NW>;
+  constexpr int kFzBS = FS::BS, kFzTile = FS::TILE, kFzRC = FS::RC, GPL = FS::GPL;
   constexpr int DP = fz_dp<D>();  // lanes per row in the threshold stage
+  constexpr int RPI = 64 / DP;    // rows per iteration of the threshold stage
   constexpr int SQW = D + 3;      // per row: requests, GPU request, affinity domain, tie salt
-  static_assert(kFzRC * DP <= 64, "threshold stage: one lane per (row, dim)");
+  static_assert(DP <= 64, "threshold stage: one lane per (row, dim)");
   // the chunk's scores s + 1 (0 = infeasible): 16-bit and double-buffered
-  // (one barrier per chunk) when every score + 1 fits 16 bits, else 32-bit
-  // with a second barrier before the tile is rewritten
-  constexpr int NB = H16 ? 2 : 1, RWD = H16 ? kFzTile / 2 : kFzTile;  // buffers, words per row
+  // (one barrier per chunk) when every score + 1 fits 16 bits and the tile
+  // is 1,024 columns, else single-buffered with a second barrier before the
+  // tile is rewritten
+  constexpr int NB = H16 && NW == 8 ? 2 : 1;  // buffers
+  // A row of the LDS tile: 4-column groups of GW words (one 8- or 16-B
+  // access), one padding group after every 64: the select reads group
+  // lane + 64k in its first pass (consecutive across lanes) and the 4·GPL
+  // columns of one candidate lane (groups L + 64k) in its survivor scan,
+  // which without the padding would all sit in one LDS bank
+  constexpr int GW = H16 ? 2 : 4, NG = kFzTile / 4;
+  constexpr int RWD = (NG + NG / 64) * GW;  // words per row
+  constexpr int TB = NW == 8 ? 10 : 11;     // log2 of the tile width (tie mode 0)
   __shared__ __attribute__((aligned(16))) uint32_t ssc[NB][kFzRC][RWD];
   __shared__ uint32_t sq[kFzMaxRows][SQW];
-  __shared__ uint64_t sbuf[kFzWaves][kFzSurv];
-  __shared__ uint32_t spos[kFzTile / 4];
-  __shared__ uint32_t spos0[kFzTile / 4];  // tie mode 0: the select-phase tie bits
-  __shared__ uint8_t scand[kFzWaves][64];  // per wave: lanes whose best reached T
+  __shared__ uint64_t sbuf[NW][kFzSurv];
+  __shared__ uint32_t spos[NG + NG / 64];   // per group (padded like the tile rows)
+  __shared__ uint32_t spos0[NG + NG / 64];  // tie mode 0: the select-phase tie bits
+  __shared__ uint8_t scand[NW][64];  // per wave: lanes whose best reached T
   constexpr int RW = (2 * D + 4 + 3) & ~3;  // row record words, whole 16-B reads
-  __shared__ __attribute__((aligned(16))) uint32_t srec[kFzWaves][kFzRC][RW];
+  __shared__ __attribute__((aligned(16))) uint32_t srec[NW][kFzRC][RW];
+  auto pgi = [](int g) { return g + (g >> 6); };  // padded group index
   if (rows_dev) fit_rows(*rows_dev, min_rpb, rows, rows_per_block);
   const int r0 = blockIdx.y * rows_per_block;
   if (r0 >= rows) return;  // block-uniform
@@ -192,6 +212,9 @@ void k_score_topk(
   (void)prof;
 #endif
   const int tile0 = tile * kFzTile;
+  // this lane's word (H16) / 8-B pair (32-bit scores) of a tile row, padded:
+  // the lane's 2 columns are half of group (wave*64 + lane) / 2
+  const int wix = (wave * 64 + lane) + 2 * ((wave * 64 + lane) >> 7);
   const int g = sp.gpu_dim;
   const int K = sp.n_cand;
   for (int i = tid; i < nr * SQW; i += kFzBS) {
@@ -254,11 +277,11 @@ void k_score_topk(
   // Monotone in the exact key, so the survivor bound stays exact; padding
   // columns wrap mod 1024 and stay below 1 << ksh.
   const bool tie0 = !sp.tie_rotated;
-  if (tid < kFzTile / 4) {
+  if (tid < NG) {
     const int c = tile0 + 4 * tid;
     const uint32_t pos = (uint32_t)(c - wshift[c >> 7]);
-    spos[tid] = pos * mul;
-    spos0[tid] = pos << 22;
+    spos[pgi(tid)] = pos * mul;
+    spos0[pgi(tid)] = pos << (32 - TB);
   }
   KP_FZ_PROF_MARK(0);
   __syncthreads();  // requests and positions staged
@@ -271,12 +294,13 @@ void k_score_topk(
   const int rsh = 32 - tbits;  // select-phase tie bits: tbits <= ksh (= ksh but in tests)
   for (int c0 = 0; c0 < nr; c0 += kFzRC) {
     const int cr = min(kFzRC, nr - c0);
-    const int buf = H16 ? (c0 / kFzRC) & 1 : 0;
+    const int buf = NB == 2 ? (c0 / kFzRC) & 1 : 0;
     // 1a. the thresholds of this wave's class: lane -> (row lane/DP, dim
     //     lane%DP), into the wave's LDS row records [q (dim 0: q + 1), GPU
     //     request, affinity domain, thresholds, WQ, GPU-fit bonus]
-    {
-      const int rr = lane / DP, d = lane % DP;
+#pragma unroll
+    for (int rb = 0; rb < kFzRC; rb += RPI) {
+      const int rr = rb + lane / DP, d = lane % DP;
       uint32_t *rec = srec[wave][rr];
       uint32_t tthr = 0xFFFFFFFFu, twq = 0, tok = 1u;
       if (rr < cr && d < D) {
@@ -377,9 +401,9 @@ void k_score_topk(
             sv[k] = mn >= 0 ? sc : 0;  // s + 1, 0 = infeasible
           }
           if constexpr (H16)
-            ssc[buf][i][wave * 64 + lane] = (uint32_t)sv[0] | ((uint32_t)sv[1] << 16);
+            ssc[buf][i][wix] = (uint32_t)sv[0] | ((uint32_t)sv[1] << 16);
           else
-            reinterpret_cast<int2 *>(ssc[0][i])[wave * 64 + lane] = make_int2(sv[0], sv[1]);
+            reinterpret_cast<int2 *>(ssc[0][i])[wix] = make_int2(sv[0], sv[1]);
         };
         using T_ = std::true_type;
         using F_ = std::false_type;
@@ -390,9 +414,9 @@ void k_score_topk(
         if constexpr (D == 4) hi0 = (cur[2] | cur[3]) == 0u;
         if (cur[0] == 0x7FFFFFFFu) {  // no column of this class fits the row
           if constexpr (H16)
-            ssc[buf][i][wave * 64 + lane] = 0u;
+            ssc[buf][i][wix] = 0u;
           else
-            reinterpret_cast<int2 *>(ssc[0][i])[wave * 64 + lane] = make_int2(0, 0);
+            reinterpret_cast<int2 *>(ssc[0][i])[wix] = make_int2(0, 0);
         } else if (hasg) {  // a GPU-fit bonus implies a GPU request: all dims
           if (hasa) score(T_{}, T_{}, DA{}); else score(T_{}, F_{}, DA{});
         } else if (hi0) {
@@ -419,19 +443,19 @@ void k_score_topk(
       const uint32_t nsl = ~sq[c0 + i][D + 2];
       // select-phase tie bits: (nst - tsp[g] - j * mt) >> rsh
       const uint32_t *tsp = tie0 ? spos0 : spos;
-      const uint32_t nst = tie0 ? (spos[0] + 1023u) << 22 : nsl, mt = tie0 ? 1u << 22 : mul;
+      const uint32_t nst = tie0 ? (spos[0] + (uint32_t)(kFzTile - 1)) << (32 - TB) : nsl,
+                     mt = tie0 ? 1u << (32 - TB) : mul;
       // lane L's 16 columns are the 4 groups 4L .. 4L + 3 (contiguous, so the
       // survivor scan below reads one candidate lane's columns from 16
       // consecutive LDS entries), visited in an order rotated by lane / 8
       // (lane / 4 for 16-B groups): the lanes of one LDS access then cover
       // every bank once (a plain 4L + k order would be 4-way conflicted)
-      constexpr int RSH = H16 ? 3 : 2;
       uint32_t best = 0;
 #pragma unroll 1
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < GPL; ++k) {
         uint32_t v4[4];
-        const int gk = 4 * lane + ((k + (lane >> RSH)) & 3);
-        load_group<H16>(ssc[buf][i], gk, v4);
+        const int gk = pgi(lane + 64 * k);  // lane L: groups L + 64k (strided: the
+        load_group<H16>(ssc[buf][i], gk, v4);  // tile's best keys spread over the lanes)
         const uint32_t npk = nst - tsp[gk];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -465,13 +489,14 @@ void k_score_topk(
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       const uint32_t *srow = ssc[buf][i];
       int C = 0;
-      for (int e0 = 0; e0 < 16 * m; e0 += 64) {  // wave-uniform
+      constexpr int CPL = 4 * GPL;  // columns per lane
+      for (int e0 = 0; e0 < CPL * m; e0 += 64) {  // wave-uniform
         const int e = e0 + lane;
         bool hit = false;
         uint32_t s1 = 0, ntk = 0;
-        if (e < 16 * m) {
-          const int L = scand[wave][e >> 4];          // candidate lane
-          const int g = 4 * L + ((e >> 2) & 3), jj = e & 3;  // its column group, column
+        if (e < CPL * m) {
+          const int L = scand[wave][e / CPL];          // candidate lane
+          const int g = pgi(L + 64 * ((e >> 2) & (GPL - 1))), jj = e & 3;  // its column group, column
           s1 = load_one<H16>(srow, 4 * g + jj);
           ntk = nsl - spos[g] - (uint32_t)jj * mul;
           hit = ((s1 << ksh) | ((nst - tsp[g] - (uint32_t)jj * mt) >> rsh)) >= T;
@@ -491,10 +516,10 @@ void k_score_topk(
           const uint64_t cb = pre | (1ull << bb);
           int c = 0;
 #pragma unroll 1
-          for (int e = 0; e < 16; ++e) {
+          for (int e = 0; e < CPL; ++e) {
             const int k = e >> 2, j = e & 3;
-            const uint32_t s1 = load_one<H16>(srow, 4 * (4 * lane + k) + j);
-            const uint32_t ntk = nsl - spos[4 * lane + k] - (uint32_t)j * mul;
+            const uint32_t s1 = load_one<H16>(srow, 4 * pgi(lane + 64 * k) + j);
+            const uint32_t ntk = nsl - spos[pgi(lane + 64 * k)] - (uint32_t)j * mul;
             c += (s1 != 0u && (((uint64_t)(0x80000000u | (s1 - 1u)) << 32) | ntk) >= cb) ? 1 : 0;
           }
           c = (int)rl((uint32_t)wave_incl_scan_i32(c), 63);
@@ -502,10 +527,10 @@ void k_score_topk(
         }
         C = 0;
 #pragma unroll 1
-        for (int e = 0; e < 16; ++e) {
+        for (int e = 0; e < CPL; ++e) {
           const int k = e >> 2, j = e & 3;
-          const uint32_t s1 = load_one<H16>(srow, 4 * (4 * lane + k) + j);
-          const uint32_t ntk = nsl - spos[4 * lane + k] - (uint32_t)j * mul;
+          const uint32_t s1 = load_one<H16>(srow, 4 * pgi(lane + 64 * k) + j);
+          const uint32_t ntk = nsl - spos[pgi(lane + 64 * k)] - (uint32_t)j * mul;
           const uint64_t key = ((uint64_t)(0x80000000u | (s1 - 1u)) << 32) | ntk;
           const bool hit = s1 != 0u && key >= pre;
           const uint64_t m = __ballot(hit);
@@ -554,7 +579,7 @@ void k_score_topk(
       }
     }
     KP_FZ_PROF_MARK(8);
-    if constexpr (!H16) __syncthreads();  // the single LDS tile is rewritten next
+    if constexpr (NB == 1) __syncthreads();  // the single LDS tile is rewritten next
   }
   KP_FZ_PROF_FLUSH();
 }
@@ -628,16 +653,18 @@ __global__ __launch_bounds__(64 * KP_MERGE_WPB) void k_merge_tour(ScoreParams sp
 
 template <int D>
 struct TopkL {
-  static int run(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
-                 int32_t ksh, int32_t *cand, const int32_t *rows_dev, bool init_wgs) {
-    const int P = c->fz_P, ntiles = P / kFzTile;
+  template <int NW>
+  static int run_nw(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
+                    int32_t ksh, int32_t *cand, const int32_t *rows_dev, bool init_wgs) {
+    using FS = FzShape<NW>;
+    const int P = c->fz_P, ntiles = P / FS::TILE;
     const int64_t want = ((int64_t)rows * ntiles + c->fz_wg_target - 1) / c->fz_wg_target;
-    const int rpb = (int)std::min<int64_t>(kFzMaxRows, std::max<int64_t>(kFzRC, want));
+    const int rpb = (int)std::min<int64_t>(kFzMaxRows, std::max<int64_t>(FS::RC, want));
     const dim3 grid(ntiles, blocks(rows, rpb));
     const int32_t tb = c->fz_tie_bits > 0 ? std::min(ksh, c->fz_tie_bits) : ksh;
-#define KP_FZ(M, H)                                                                              \
-  hipLaunchKernelGGL((k_score_topk<D, M, H>), grid, dim3(kFzBS), 0, c->stream, sp, c->d.np32, P, \
-                     c->d.q, c->U, c->d.aff, c->d.salt, rows_unit, rows, rpb, kFzRC, rows_dev,    \
+#define KP_FZ(M, H)                                                                               \
+  hipLaunchKernelGGL((k_score_topk<D, M, H, NW>), grid, dim3(FS::BS), 0, c->stream, sp, c->d.np32, \
+                     P, c->d.q, c->U, c->d.aff, c->d.salt, rows_unit, rows, rpb, FS::RC, rows_dev,  \
                      c->d.wshift, ksh, tb, c->d.part, c->d.fz_prof)
     // 16-bit LDS scores when every score + 1 < 2^16 (ksh >= 16)
     const bool h16 = ksh >= 16 && c->fz_h16;
@@ -673,6 +700,10 @@ struct TopkL {
 #undef KP_MG
     KP_HIP(hipGetLastError());
     return KP_OK;
+  }
+  static int run(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
+                 int32_t ksh, int32_t *cand, const int32_t *rows_dev, bool init_wgs) {
+    return run_nw<kFzWaves>(c, sp, rows_unit, rows, ksh, cand, rows_dev, init_wgs);
   }
 };
 

@@ -5,7 +5,7 @@
 set -e
 REPO=$(cd "$(dirname "$0")/.." && pwd)
 PKG=kubernetes-native-distributed-ai-job-scheduler_amd
-OUT=$REPO/$PKG/build/ab
+OUT=${ABOUT:-$REPO/$PKG/build/ab}
 mkdir -p "$OUT"
 WT=$(mktemp -d /tmp/kpwt.XXXX)
 if [ "$1" = WORKTREE ]; then
