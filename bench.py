@@ -60,6 +60,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # VALU peak for 32-bit integer ops: 256 CUs x 4 SIMDs x 32 lanes/cycle (a wave64
 # VALU op issues over 2 cycles on a SIMD-32, MI355X_MICROARCH.md) x 2.4 GHz
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+# measured: independent v_add_u32 / compare-select / sub-min chains on every
+# SIMD issue ~56 T lane-ops/s (tools/valu_peak.hip, profiles/r05_valu_peak.txt:
+# 32 lanes per clock at the ~1.7 GHz the chip holds under that load)
+VALU_ACHIEVABLE_TOPS = 56.4
 
 
 def progress(msg: str) -> None:
@@ -564,7 +568,7 @@ def main():
     fused = bool(tm["fused"])
     kname = "k_score_topk" if fused else "k_score32"
     traffic, traffic_src, valu = None, None, None
-    for pmc in ("r04_pmc.json", "r03_pmc.json", "r02_pmc.json", "r01_pmc.json"):  # HBM-side bytes per launch (rocprofv3 PMC), newest first
+    for pmc in ("r05_pmc.json", "r04_pmc.json", "r03_pmc.json", "r02_pmc.json", "r01_pmc.json"):  # HBM-side bytes per launch (rocprofv3 PMC), newest first
         path = os.path.join(REPO, "profiles", pmc)
         if os.path.exists(path):
             with open(path) as f:
@@ -579,7 +583,7 @@ def main():
         # judged on pairs/s and on the VALU roofline (lane-ops per pair from
         # the SQ_INSTS_VALU counter of the same solve, profiles/r0N_valu.json)
         opp, vsrc = None, None
-        for vj in ("r04_valu.json", "r03_valu.json", "r02_valu.json"):  # newest evidence first
+        for vj in ("r05_valu.json", "r04_valu.json", "r03_valu.json", "r02_valu.json"):  # newest evidence first
             path = os.path.join(REPO, "profiles", vj)
             if os.path.exists(path):
                 with open(path) as f:
@@ -596,6 +600,9 @@ def main():
         if opp:
             valu["achieved"] = kpairs * opp / 1e12
             valu["frac"] = valu["achieved"] / VALU_PEAK_TOPS
+            valu["achievable"] = VALU_ACHIEVABLE_TOPS
+            valu["frac_of_achievable"] = valu["achieved"] / VALU_ACHIEVABLE_TOPS
+            valu["achievable_source"] = "tools/valu_peak.hip (profiles/r05_valu_peak.txt)"
     out = {
         "metric": METRIC,
         "value": pairs / (ms / 1e3),

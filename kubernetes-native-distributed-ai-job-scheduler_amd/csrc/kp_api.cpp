@@ -332,6 +332,7 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = knob("KP_SELECT_LDS_CAP")) c->select_lds_cap = std::atoi(e);
   if (const char *e = knob("KP_SELECT_GENERIC")) c->select_generic = std::atoi(e) != 0;
   if (const char *e = knob("KP_SELECT_BS")) c->select_bs = std::atoi(e);
+  if (const char *e = knob("KP_FZ_CREC")) c->crec_enabled = std::atoi(e) != 0;
   if (const char *e = knob("KP_SCORE_WG_TARGET")) c->score_wg_target = std::max(64, std::atoi(e));
   if (const char *e = knob("KP_SCORE_MIN_RPB")) c->score_min_rpb = std::max(1, std::atoi(e));
   if (const char *e = knob("KP_SCORE_NPL")) c->score_npl = std::atoi(e) == 4 ? 4 : 2;
@@ -469,6 +470,34 @@ static int load_nodes_impl(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap,
     return fail(KP_ENOMEM, "kp_load_nodes: host copy");
   }
   const int32_t fz_P = (int32_t)colnode.size();
+  // the fused layout's classes: per wave tile its class, per class its
+  // capacity vector (32-bit: the fused path needs every cap < 2^30)
+  std::vector<int32_t> tcls;
+  std::vector<uint32_t> fccap;
+  try {
+    if (fz_P > 0) {
+      tcls.assign((size_t)fz_P / 128, 0);
+      int32_t k = 0;
+      int64_t col = 0;
+      for (int32_t i = 0; i < N; ++k) {
+        int32_t e = i + 1;
+        while (e < N && [&] {
+          for (int d = 0; d < D; ++d)
+            if (cap[(int64_t)d * N + c->h_perm[e]] != cap[(int64_t)d * N + c->h_perm[i]]) return false;
+          return true;
+        }()) ++e;
+        col = (col + 127) & ~(int64_t)127;
+        for (int64_t t = col; t < col + (e - i); t += 128) tcls[(size_t)(t / 128)] = k;
+        col += e - i;
+        for (int d = 0; d < D; ++d)
+          fccap.push_back((uint32_t)std::min<int64_t>(cap[(int64_t)d * N + c->h_perm[i]], 0xFFFFFFFFll));
+        i = e;
+      }
+    }
+  } catch (const std::bad_alloc &) {
+    return fail(KP_ENOMEM, "kp_load_nodes: host copy");
+  }
+  const int32_t nfc = (int32_t)(fccap.size() / std::max(D, 1));
   // capacity classes for k_score32's class form: the runs of equal capacity
   // vectors in canonical order (at most kScoreClasses of them)
   std::vector<uint32_t> ncls, ccap;
@@ -510,7 +539,14 @@ static int load_nodes_impl(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap,
                           hipMemcpyHostToDevice, c->stream));
     KP_HIP(hipMemcpyAsync(c->d.wshift, wshift.data(), sizeof(int32_t) * (fz_P / 128),
                           hipMemcpyHostToDevice, c->stream));
+    KP_TRY(dalloc(&c->d.tcls, (size_t)fz_P / 128));
+    KP_TRY(dalloc(&c->d.fccap, std::max<size_t>(fccap.size(), 1)));
+    KP_HIP(hipMemcpyAsync(c->d.tcls, tcls.data(), sizeof(int32_t) * (fz_P / 128),
+                          hipMemcpyHostToDevice, c->stream));
+    KP_HIP(hipMemcpyAsync(c->d.fccap, fccap.data(), sizeof(uint32_t) * fccap.size(),
+                          hipMemcpyHostToDevice, c->stream));
   }
+  c->nfc = fz_P > 0 ? nfc : 0;
   if (N > 0) {
     KP_HIP(hipMemcpyAsync(c->d.cap, c->h_cap.data(), sizeof(int64_t) * D * N,
                           hipMemcpyHostToDevice, c->stream));
@@ -828,7 +864,21 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   c->pack_full = true;
   c->last_fused = fused;
   int64_t rpc = rows_per_chunk(c);
+  c->crec_ok = false;
   if (fused) {
+    // the row records of every unit and class, once for the whole solve
+    // (they depend on the requests and the class capacities, not on usage)
+    const int RWr = (2 * c->D + 4 + 3) & ~3;
+    const int64_t words = (int64_t)std::max(U, 1) * std::max(c->nfc, 1) * RWr;
+    if (c->nfc > 0 && c->crec_enabled && words * 4 <= c->crec_max_bytes) {
+      if (words > c->cap_crec) {
+        c->cap_crec = 0;
+        KP_TRY(dalloc(&c->d.crec, (size_t)words));
+        c->cap_crec = words;
+      }
+      KP_TRY(launch_unit_rec(c, sp));
+      c->crec_ok = true;
+    }
     rpc = INT64_MAX;  // no matrix, no chunks: per row only tiles x K keys
     KP_TRY(ensure_part(c, (int64_t)std::max(shard, 1) * (c->fz_P / fz_tile(c)) * K));
     if (!c->d.part || !c->d.colnode || !c->d.wshift)
@@ -1356,7 +1406,7 @@ void kp_destroy(kp_ctx *c) {
                   d.temp, d.xg_counts, d.xg_send, d.xg_recv, d.uprio, d.plist, d.pre_send, d.pre_recv, d.roff,
                   d.rreq, d.rsuf, d.rprio, d.pre_node, d.pre_vict, d.pre_cost,
                   d.dl_node, d.dl_delta, d.dl_bad, d.node_flag, d.node_list, d.nrec, d.nst, d.stats, d.np32, d.ncls, d.ccap, d.colnode, d.wshift, d.part, d.fz_prof,
-                  d.bm, d.bms, d.rowinfo, d.cnt, d.rowmap};
+                  d.bm, d.bms, d.rowinfo, d.cnt, d.rowmap, d.tcls, d.fccap, d.crec};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->world > 1) {

@@ -98,6 +98,12 @@ struct DevState {
   // column (pos = column - wshift[column / 128])
   int32_t *colnode = nullptr;  // [fz_P]
   int32_t *wshift = nullptr;   // [fz_P / 128]
+  // fused solve: capacity class of every 128-column wave tile ([fz_P / 128],
+  // 0 for padding-only tiles), the classes' capacities ([nfc][D]) and the
+  // per-(unit, class) row records of k_score_topk ([U][nfc][RW], once per solve)
+  int32_t *tcls = nullptr;
+  uint32_t *fccap = nullptr;
+  uint32_t *crec = nullptr;
   uint64_t *part = nullptr;    // [rows][fz_P / 1024][K] per-tile top-K keys
   uint64_t *fz_prof = nullptr; // [16] phase clocks of a KP_FZ_PROFILE build (KP_FZ_PROF=1)
   // units (rank order), job outputs
@@ -259,6 +265,11 @@ struct kp_ctx {
   int64_t max_cap = 0, max_req = 0;  // largest cap / request of the loaded tables
   int32_t cap_mask_rows = 0;   // rows of d.mask (kp_score only)
   int64_t cap_rowmap = 0;      // entries of d.rowmap (kp_score_dev only)
+  int32_t nfc = 0;             // capacity classes of the fused layout (d.fccap)
+  int64_t cap_crec = 0;        // words of d.crec
+  bool crec_ok = false;        // this solve's row records are in d.crec (k_score_topk PRE form)
+  bool crec_enabled = true;    // KP_FZ_CREC=0: thresholds inside k_score_topk (A/B)
+  int64_t crec_max_bytes = (int64_t)512 << 20;  // larger tables: in-kernel thresholds
   int64_t cap_q = 0;           // int64 entries of d.q
   int32_t u_lo = 0, u_hi = 0;  // this rank's shard of units (rank positions)
   bool nodes_loaded = false, jobs_loaded = false, solved = false;
@@ -336,6 +347,9 @@ int launch_select(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit,
 // `rows` rows (act_local order) straight into cand, no score matrix
 // (init_wgs: the merge's extra workgroups re-initialise the round state when
 // it does k_csr_keys' work)
+// the per-(unit, class) row records of the fused candidate phase (thresholds
+// c - rho, WQ and the row's request / GPU / affinity words), once per solve
+int launch_unit_rec(kp_ctx *c, const ScoreParams &sp);
 int launch_score_topk(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
                       int32_t ksh, int32_t *cand, const int32_t *rows_dev, bool init_wgs);
 int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev = nullptr);

@@ -742,8 +742,16 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
   }
 }
 
+#ifndef KP_PLAN_WPE
+#define KP_PLAN_WPE 0  // >0: waves per SIMD the plan's register budget must allow (A/B build knob;
+                       // 7 and 8 measured slower in r05: spills, config #4 +3 / +20 ms)
+#endif
 template <int D, int G, bool W32>
-__global__ __launch_bounds__(64 * KP_PLAN_WPB) void k_plan(PlanArgs pa) {
+__global__ __launch_bounds__(64 * KP_PLAN_WPB)
+#if KP_PLAN_WPE > 0
+__attribute__((amdgpu_waves_per_eu(KP_PLAN_WPE, KP_PLAN_WPE)))
+#endif
+void k_plan(PlanArgs pa) {
   if (pa.pass == 0 && pa.csr_count) {
     // window w = this wave (the grid has >= ceil(A*K/64) waves): the smallest
     // request per dim over its entries, a lower bound for k_accept's pruning

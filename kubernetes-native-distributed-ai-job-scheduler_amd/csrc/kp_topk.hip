@@ -163,7 +163,7 @@ __device__ __forceinline__ uint32_t load_one(const uint32_t *row, int col) {
 #ifndef KP_FZ_WAVES_PER_EU
 #define KP_FZ_WAVES_PER_EU 6  // NW = 8: 80 VGPRs, 3 workgroups of 8 waves per CU (a small spill is cheaper than 2)
 #endif
-template <int D, bool MOST, bool H16, int NW>
+template <int D, bool MOST, bool H16, int NW, bool PRE>
 __global__ __launch_bounds__(64 * NW)
 __attribute__((amdgpu_waves_per_eu(NW == 8 ? KP_FZ_WAVES_PER_EU : 4, NW == 8 ? KP_FZ_WAVES_PER_EU : 4)))
 void k_score_topk(
@@ -171,7 +171,8 @@ void k_score_topk(
     int32_t qstride, const int32_t *__restrict__ uaff, const uint32_t *__restrict__ salt,
     const int32_t *__restrict__ rows_unit, int32_t rows, int32_t rows_per_block, int32_t min_rpb,
     const int32_t *__restrict__ rows_dev, const int32_t *__restrict__ wshift, int32_t ksh, int32_t tbits,
-    uint64_t *__restrict__ part, uint64_t *__restrict__ prof) {
+    uint64_t *__restrict__ part, uint64_t *__restrict__ prof, const uint32_t *__restrict__ crec,
+    const int32_t *__restrict__ tcls, int32_t nfc) {
   using FS = FzShape<NW>;
   constexpr int kFzBS = FS::BS, kFzTile = FS::TILE, kFzRC = FS::RC, GPL = FS::GPL;
   constexpr int DP = fz_dp<D>();  // lanes per row in the threshold stage
@@ -199,6 +200,7 @@ void k_score_topk(
   __shared__ uint8_t scand[NW][64];  // per wave: lanes whose best reached T
   constexpr int RW = (2 * D + 4 + 3) & ~3;  // row record words, whole 16-B reads
   __shared__ __attribute__((aligned(16))) uint32_t srec[NW][kFzRC][RW];
+  __shared__ int32_t su[PRE ? kFzMaxRows : 1];  // PRE: the rows' units
   auto pgi = [](int g) { return g + (g >> 6); };  // padded group index
   if (rows_dev) fit_rows(*rows_dev, min_rpb, rows, rows_per_block);
   const int r0 = blockIdx.y * rows_per_block;
@@ -217,19 +219,27 @@ void k_score_topk(
   const int wix = (wave * 64 + lane) + 2 * ((wave * 64 + lane) >> 7);
   const int g = sp.gpu_dim;
   const int K = sp.n_cand;
-  for (int i = tid; i < nr * SQW; i += kFzBS) {
-    const int rr = i / SQW, d = i - rr * SQW;
-    const int32_t unit = rows_unit[r0 + rr];
-    uint32_t v;
-    if (d == D + 2) {
-      v = sp.tie_rotated ? salt[unit] : 0u;
-    } else if (d == D + 1) {
-      v = (uint32_t)uaff[unit];
-    } else {
-      const int dd = d < D ? d : g;
-      v = dd >= 0 ? (uint32_t)q[(int64_t)dd * qstride + unit] : 0u;
+  if constexpr (PRE) {  // the row records come precomputed: units and tie salts only
+    for (int i = tid; i < nr; i += kFzBS) {
+      const int32_t unit = rows_unit[r0 + i];
+      su[i] = unit;
+      sq[i][D + 2] = sp.tie_rotated ? salt[unit] : 0u;
     }
-    sq[rr][d] = v;
+  } else {
+    for (int i = tid; i < nr * SQW; i += kFzBS) {
+      const int rr = i / SQW, d = i - rr * SQW;
+      const int32_t unit = rows_unit[r0 + rr];
+      uint32_t v;
+      if (d == D + 2) {
+        v = sp.tie_rotated ? salt[unit] : 0u;
+      } else if (d == D + 1) {
+        v = (uint32_t)uaff[unit];
+      } else {
+        const int dd = d < D ? d : g;
+        v = dd >= 0 ? (uint32_t)q[(int64_t)dd * qstride + unit] : 0u;
+      }
+      sq[rr][d] = v;
+    }
   }
   // the wave's 128 columns: 2 per lane, one 8-B load per plane
   const uint2 *pv = reinterpret_cast<const uint2 *>(np);
@@ -292,9 +302,28 @@ void k_score_topk(
   for (int d = 0; d < D; ++d) wv[d] = in_vgpr(sp.w[d]);
   const int32_t waffv = in_vgpr(sp.w_affinity);
   const int rsh = 32 - tbits;  // select-phase tie bits: tbits <= ksh (= ksh but in tests)
+  // PRE: this wave's class and its row records (kp_score.hip k_unit_rec), RW/4
+  // 16-B pieces per row, one per lane, the next chunk's loaded while the
+  // current one is scored
+  constexpr int Q4 = RW / 4;
+  static_assert(!PRE || kFzRC * Q4 <= 64, "one record piece per lane");
+  const int cls = PRE ? tcls[(tile0 >> 7) + wave] : 0;
+  const uint4 *crec4 = reinterpret_cast<const uint4 *>(crec);
+  uint4 nx = make_uint4(0u, 0u, 0u, 0u);
+  if (PRE && lane < min(kFzRC, nr) * Q4)
+    nx = crec4[((int64_t)su[lane / Q4] * nfc + cls) * Q4 + lane % Q4];
   for (int c0 = 0; c0 < nr; c0 += kFzRC) {
     const int cr = min(kFzRC, nr - c0);
     const int buf = NB == 2 ? (c0 / kFzRC) & 1 : 0;
+    if constexpr (PRE) {  // 1a. the chunk's row records: one 16-B piece per lane
+      if (lane < cr * Q4) reinterpret_cast<uint4 *>(srec[wave][lane / Q4])[lane % Q4] = nx;
+      const int c1 = c0 + kFzRC;
+      if (lane < min(kFzRC, nr - c1) * Q4)
+        nx = crec4[((int64_t)su[c1 + lane / Q4] * nfc + cls) * Q4 + lane % Q4];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else
     // 1a. the thresholds of this wave's class: lane -> (row lane/DP, dim
     //     lane%DP), into the wave's LDS row records [q (dim 0: q + 1), GPU
     //     request, affinity domain, thresholds, WQ, GPU-fit bonus]
@@ -588,7 +617,48 @@ void k_score_topk(
 // holds the heads of lists t, t+64, ... (LPL per lane); K times the wave
 // max of the heads, and only the owner of the max advances its list (one LDS
 // read). K x (one wave max + one LDS read) per row instead of K passes over
-// all ntiles*K keys. Dynamic LDS: 4 rows x ntiles*K keys.
+// all ntiles*K keys. Returns the canonical position of candidate `lane`
+// (-1 past the row's feasible nodes). L = the row's lists in LDS.
+template <int LPL>
+__device__ __forceinline__ int32_t merge_tour_row(const uint64_t *L, int32_t ntiles, int32_t K,
+                                                  uint32_t sl, uint32_t inv, int lane) {
+  int h[LPL];
+  uint64_t v[LPL];
+#pragma unroll
+  for (int j = 0; j < LPL; ++j) {
+    const int t = lane + 64 * j;
+    h[j] = 0;
+    v[j] = t < ntiles ? L[t * K] : 0ull;
+  }
+  // lane it keeps the canonical position of candidate it; the positions are
+  // mapped to nodes after the loop with ONE load per lane (a perm load + store
+  // inside the loop serialises K memory latencies)
+  int32_t mypos = -1;
+  for (int it = 0; it < K; ++it) {
+    uint64_t b = v[0];
+#pragma unroll
+    for (int j = 1; j < LPL; ++j) b = v[j] > b ? v[j] : b;
+    const uint32_t mhi = wave_max32((uint32_t)(b >> 32));
+    const uint32_t mlo = wave_max32((uint32_t)(b >> 32) == mhi ? (uint32_t)b : 0u);
+    const uint64_t m = ((uint64_t)mhi << 32) | mlo;
+    if (m == 0) break;  // fewer than K feasible nodes: lanes >= it keep -1
+#pragma unroll
+    for (int j = 0; j < LPL; ++j)
+      if (v[j] == m) {  // keys are unique: one list of one lane
+        const int t = lane + 64 * j;
+        ++h[j];
+        v[j] = h[j] < K ? L[t * K + h[j]] : 0ull;
+      }
+    if (lane == it) mypos = key_node(m, sl, inv);
+  }
+  return mypos;
+}
+
+// One wave per row: the row's ntiles sorted per-tile lists staged in LDS and
+// merged by the tournament; the candidates' canonical positions mapped to
+// nodes through perm. Dynamic LDS: KP_MERGE_WPB rows x ntiles*K keys. (A
+// threshold merge — T = the largest K-th key of the tile lists, the keys >= T
+// ranked exactly — measured equal in r05 and was dropped.)
 template <int LPL>
 __global__ __launch_bounds__(64 * KP_MERGE_WPB) void k_merge_tour(ScoreParams sp, const uint64_t *__restrict__ part,
                                                     int32_t ntiles,
@@ -613,38 +683,10 @@ __global__ __launch_bounds__(64 * KP_MERGE_WPB) void k_merge_tour(ScoreParams sp
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  int h[LPL];
-  uint64_t v[LPL];
-#pragma unroll
-  for (int j = 0; j < LPL; ++j) {
-    const int t = lane + 64 * j;
-    h[j] = 0;
-    v[j] = t < ntiles ? L[t * K] : 0ull;
-  }
   const int32_t unit = rows_unit[row];
   const uint32_t sl = sp.tie_rotated ? salt[unit] : 0u;
   const uint32_t inv = sp.tie_rotated ? kTieMulInv : 1u;
-  // lane it keeps the canonical position of candidate it; the positions are
-  // mapped to nodes after the loop with ONE load per lane (a perm load + store
-  // inside the loop serialises K memory latencies)
-  int32_t mypos = -1;
-  for (int it = 0; it < K; ++it) {
-    uint64_t b = v[0];
-#pragma unroll
-    for (int j = 1; j < LPL; ++j) b = v[j] > b ? v[j] : b;
-    const uint32_t mhi = wave_max32((uint32_t)(b >> 32));
-    const uint32_t mlo = wave_max32((uint32_t)(b >> 32) == mhi ? (uint32_t)b : 0u);
-    const uint64_t m = ((uint64_t)mhi << 32) | mlo;
-    if (m == 0) break;  // fewer than K feasible nodes: lanes >= it keep -1
-#pragma unroll
-    for (int j = 0; j < LPL; ++j)
-      if (v[j] == m) {  // keys are unique: one list of one lane
-        const int t = lane + 64 * j;
-        ++h[j];
-        v[j] = h[j] < K ? L[t * K + h[j]] : 0ull;
-      }
-    if (lane == it) mypos = key_node(m, sl, inv);
-  }
+  const int32_t mypos = merge_tour_row<LPL>(L, ntiles, K, sl, inv, lane);
   // canonical position -> node (a position is always < N)
   const int32_t mine = (uint32_t)mypos < (uint32_t)sp.N ? perm[mypos] : -1;
   if (lane < K) cand[(int64_t)row * K + lane] = mine;
@@ -662,10 +704,15 @@ struct TopkL {
     const int rpb = (int)std::min<int64_t>(kFzMaxRows, std::max<int64_t>(FS::RC, want));
     const dim3 grid(ntiles, blocks(rows, rpb));
     const int32_t tb = c->fz_tie_bits > 0 ? std::min(ksh, c->fz_tie_bits) : ksh;
-#define KP_FZ(M, H)                                                                               \
-  hipLaunchKernelGGL((k_score_topk<D, M, H, NW>), grid, dim3(FS::BS), 0, c->stream, sp, c->d.np32, \
-                     P, c->d.q, c->U, c->d.aff, c->d.salt, rows_unit, rows, rpb, FS::RC, rows_dev,  \
-                     c->d.wshift, ksh, tb, c->d.part, c->d.fz_prof)
+#define KP_FZ_(M, H, PR)                                                                             \
+  hipLaunchKernelGGL((k_score_topk<D, M, H, NW, PR>), grid, dim3(FS::BS), 0, c->stream, sp, c->d.np32, \
+                     P, c->d.q, c->U, c->d.aff, c->d.salt, rows_unit, rows, rpb, FS::RC, rows_dev,      \
+                     c->d.wshift, ksh, tb, c->d.part, c->d.fz_prof, c->d.crec, c->d.tcls, c->nfc)
+#define KP_FZ(M, H)          \
+  if (c->crec_ok)            \
+    KP_FZ_(M, H, true);      \
+  else                       \
+    KP_FZ_(M, H, false)
     // 16-bit LDS scores when every score + 1 < 2^16 (ksh >= 16)
     const bool h16 = ksh >= 16 && c->fz_h16;
     if (sp.most_allocated) {
@@ -674,6 +721,7 @@ struct TopkL {
       if (h16) KP_FZ(false, true); else KP_FZ(false, false);
     }
 #undef KP_FZ
+#undef KP_FZ_
     KP_HIP(hipGetLastError());
     if (c->fz_end_event) KP_HIP(hipEventRecord(c->fz_end_event, c->stream));
     const int M = ntiles * sp.n_cand;
@@ -707,7 +755,71 @@ struct TopkL {
   }
 };
 
+// Row records of the fused candidate phase, once per solve: for unit u and
+// fused capacity class k (capacities c_d), the words k_score_topk's stage 1a
+// computed per chunk and wave before — [q_0 + 1 (0x7FFFFFFF: no column of
+// the class fits), q_1 .. q_{D-1}, GPU request, affinity domain, thresholds
+// c_d - rho_d (q_d·S = Q_d·c_d + rho_d; 0xFFFFFFFF: cap-0 dim or q > c),
+// WQ = sum_d w_d·Q_d, GPU-fit bonus] — with exact 64-bit divisions.
+template <int D>
+__global__ void k_unit_rec(ScoreParams sp, const int64_t *__restrict__ q, int32_t U,
+                           const int32_t *__restrict__ uaff, const uint32_t *__restrict__ fccap,
+                           int32_t nfc, uint32_t *__restrict__ crec) {
+  constexpr int RW = (2 * D + 4 + 3) & ~3;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)U * nfc) return;
+  const int32_t u = (int32_t)(t / nfc), k = (int32_t)(t - (int64_t)u * nfc);
+  uint32_t rec[RW];
+#pragma unroll
+  for (int i = 0; i < RW; ++i) rec[i] = 0u;
+  const uint64_t S = (uint64_t)sp.S;
+  uint32_t wq = 0;
+  bool ok = true;
+  uint32_t q0 = 0;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const uint32_t qd = (uint32_t)q[(int64_t)d * U + u], c = fccap[(int64_t)k * D + d];
+    uint32_t thr = 0xFFFFFFFFu;
+    if (c == 0u) {
+      ok &= qd == 0u;
+    } else if (qd > c) {
+      ok = false;
+    } else {
+      const uint64_t x = (uint64_t)qd * S, Q = x / c;
+      thr = c - (uint32_t)(x - Q * c);
+      wq += (uint32_t)sp.w[d] * (uint32_t)Q;
+    }
+    if (d == 0) q0 = qd;
+    else rec[d] = qd;
+    rec[D + 2 + d] = thr;
+  }
+  const int g = sp.gpu_dim;
+  const uint32_t qg = g >= 0 ? (uint32_t)q[(int64_t)g * U + u] : 0u;
+  rec[0] = ok ? q0 + 1u : 0x7FFFFFFFu;
+  rec[D] = qg;
+  rec[D + 1] = (uint32_t)uaff[u];
+  rec[2 * D + 2] = wq;
+  rec[2 * D + 3] = qg != 0u ? (uint32_t)sp.w_gpu_fit : 0u;
+  uint4 *dst = reinterpret_cast<uint4 *>(crec + t * RW);
+#pragma unroll
+  for (int i = 0; i < RW / 4; ++i) dst[i] = make_uint4(rec[4 * i], rec[4 * i + 1], rec[4 * i + 2], rec[4 * i + 3]);
+}
+
+template <int D>
+struct UnitRecL {
+  static int run(kp_ctx *c, const ScoreParams &sp) {
+    const int64_t n = (int64_t)c->U * c->nfc;
+    if (n <= 0) return KP_OK;
+    hipLaunchKernelGGL(k_unit_rec<D>, dim3(blocks(n, 256)), dim3(256), 0, c->stream, sp, c->d.q,
+                       c->U, c->d.aff, c->d.fccap, c->nfc, c->d.crec);
+    KP_HIP(hipGetLastError());
+    return KP_OK;
+  }
+};
+
 }  // namespace
+
+int launch_unit_rec(kp_ctx *c, const ScoreParams &sp) { return dispatch_D<UnitRecL>(c->D, c, sp); }
 
 int launch_score_topk(kp_ctx *c, const ScoreParams &sp, const int32_t *rows_unit, int32_t rows,
                       int32_t ksh, int32_t *cand, const int32_t *rows_dev, bool init_wgs) {

@@ -392,11 +392,15 @@ FUSED_CASES = [  # (D, score_mode, tie_mode, n_cand, N, classes)
 ]
 
 
+@pytest.mark.parametrize("crec", ["1", "0"])
 @pytest.mark.parametrize("case", range(len(FUSED_CASES)))
-def test_fused_topk_parity(oracle, case):
+def test_fused_topk_parity(oracle, monkeypatch, case, crec):
     """The fused filter + score + top-K candidate phase (no score matrix) is
     bit-exact with the oracle: dims 1..8, both score modes and tie modes,
-    K in {1..32}, partial tiles, cap-0 dims inside classes, affinity."""
+    K in {1..32}, partial tiles, cap-0 dims inside classes, affinity; with the
+    per-solve row-record table (k_unit_rec) and with the records computed
+    inside the kernel (KP_FZ_CREC=0)."""
+    monkeypatch.setenv("KP_FZ_CREC", crec)
     D, mode, tie, K, N, classes = FUSED_CASES[case]
     w = few_class_workload(500 + case, J=2500, N=N, D=D, classes=classes)
     p = _abi.default_params(score_mode=mode, tie_mode=tie, n_cand=K, gpu_dim=D - 1,
@@ -413,6 +417,8 @@ def test_fused_topk_parity(oracle, case):
     (("KP_FZ_WG_TARGET", "64"),),   # 128 rows per fused workgroup
     (("KP_FZ_WG_TARGET", "1000000"),),  # 8 rows (one chunk) per fused workgroup
     (("KP_FZ_H16", "0"),),          # 32-bit LDS scores (single buffer, two barriers)
+    (("KP_FZ_CREC", "0"),),         # row records computed inside the kernel (no per-solve table)
+    (("KP_FZ_CREC", "0"), ("KP_FZ_H16", "0")),
 ])
 def test_fused_knobs_parity(oracle, monkeypatch, knobs):
     for k, v in knobs:
