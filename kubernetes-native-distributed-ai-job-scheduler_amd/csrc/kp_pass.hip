@@ -539,6 +539,7 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
   int32_t szmax = sz;
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) szmax = max(szmax, __shfl_xor(szmax, m, kWave));
+  szmax = __builtin_amdgcn_readfirstlane(szmax);  // wave-uniform: scalar branches
   if constexpr (W32) {
     // every cap and request < 2^32 (fits32): the remaining free capacity is
     // tracked incrementally and the utilisation of one more member is
@@ -579,21 +580,31 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
     // utilisations of the winning lane.
     uint32_t cnt = valid ? 64u : 0u;
     int32_t pfit = -1;
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      if (q32[d] != 0u) {
-        const uint32_t c = floor_div_cap64(rem[d], q32[d]);
-        cnt = min(cnt, c);
-        if (d == g && (uint64_t)c * q32[d] == rem[d]) pfit = (int32_t)c - 1;
-      }
-    }
-    // the group's lanes in this lane's topo domain, bit G-1-j for lane j (the
-    // spread penalty counts members planned into the domain of the winning
-    // candidate; a lane without a valid candidate counts none)
     uint32_t rmask = 0;
+    if (szmax == 1) {
+      // singleton units only (the streaming case): one fit test, no spread
+      // penalty (it only affects later members)
 #pragma unroll
-    for (int j = 0; j < G; ++j) rmask |= (__shfl(tp, gbase + j, kWave) == tp ? 1u : 0u) << (G - 1 - j);
-    if (!valid) rmask = 0;
+      for (int d = 0; d < D; ++d) {
+        if (q32[d] > rem[d]) cnt = 0;
+        if (d == g && q32[d] != 0u && q32[d] == rem[d]) pfit = 0;
+      }
+    } else {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        if (q32[d] != 0u) {
+          const uint32_t c = floor_div_cap64(rem[d], q32[d]);
+          cnt = min(cnt, c);
+          if (d == g && (uint64_t)c * q32[d] == rem[d]) pfit = (int32_t)c - 1;
+        }
+      }
+      // the group's lanes in this lane's topo domain, bit G-1-j for lane j
+      // (the spread penalty counts members planned into the domain of the
+      // winning candidate; a lane without a valid candidate counts none)
+#pragma unroll
+      for (int j = 0; j < G; ++j) rmask |= (__shfl(tp, gbase + j, kWave) == tp ? 1u : 0u) << (G - 1 - j);
+      if (!valid) rmask = 0;
+    }
     KP_PP_MARK(1);
     // One 32-bit key per lane, (value + off) << log2 G | (G-1-lane): one group
     // max gives the best value and, among equal values, the lowest lane; key
@@ -909,13 +920,6 @@ __device__ __forceinline__ void decide_window(const Win<D, N32> &wc,
     // window is done without any prefix scan
     const uint64_t fam = __ballot(fa);
     if (fam == 0) break;
-    if ((fam & (fam - 1)) == 0) {  // one lane fits alone: it is accepted, no scans
-      const int l1 = __ffsll((unsigned long long)fam) - 1;
-      accepted |= fa;
-#pragma unroll
-      for (int d = 0; d < D; ++d) rem[d] -= readlane_nt(wc.need[d], l1);
-      break;
-    }
     bool okp = fa;
     NT pre[D];
 #pragma unroll

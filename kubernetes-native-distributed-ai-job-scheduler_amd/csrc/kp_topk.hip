@@ -59,6 +59,12 @@
   do {                     \
   } while (0)
 #endif
+#ifndef KP_FZ_DMA
+#define KP_FZ_DMA 1  // PRE row records by LDS DMA (0: through VGPRs; A/B knob)
+#endif
+#ifndef KP_FZ_RANK_UNROLL
+#define KP_FZ_RANK_UNROLL 4  // survivor rank loop unroll (A/B knob)
+#endif
 #ifndef KP_FZ_ROW_UNROLL
 #define KP_FZ_ROW_UNROLL 1  // rows of the score loop interleaved (A/B knob)
 #endif
@@ -193,13 +199,18 @@ void k_score_topk(
   constexpr int RWD = (NG + NG / 64) * GW;  // words per row
   constexpr int TB = NW == 8 ? 10 : 11;     // log2 of the tile width (tie mode 0)
   __shared__ __attribute__((aligned(16))) uint32_t ssc[NB][kFzRC][RWD];
-  __shared__ uint32_t sq[kFzMaxRows][SQW];
-  __shared__ uint64_t sbuf[NW][kFzSurv];
+  // PRE keeps only the tie salt per row (the LDS for the second record buffer)
+  constexpr int SALT = PRE ? 0 : D + 2;
+  __shared__ uint32_t sq[kFzMaxRows][PRE ? 1 : SQW];
+  __shared__ __attribute__((aligned(16))) uint64_t sbuf[NW][kFzSurv];
   __shared__ uint32_t spos[NG + NG / 64];   // per group (padded like the tile rows)
   __shared__ uint32_t spos0[NG + NG / 64];  // tie mode 0: the select-phase tie bits
   __shared__ uint8_t scand[NW][64];  // per wave: lanes whose best reached T
   constexpr int RW = (2 * D + 4 + 3) & ~3;  // row record words, whole 16-B reads
-  __shared__ __attribute__((aligned(16))) uint32_t srec[NW][kFzRC][RW];
+  // PRE + KP_FZ_DMA: two buffers, the next chunk's records copied by the
+  // memory unit straight into LDS while the current chunk is scored
+  constexpr int NRB = PRE && KP_FZ_DMA ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) uint32_t srec[NRB][NW][kFzRC][RW];
   __shared__ int32_t su[PRE ? kFzMaxRows : 1];  // PRE: the rows' units
   auto pgi = [](int g) { return g + (g >> 6); };  // padded group index
   if (rows_dev) fit_rows(*rows_dev, min_rpb, rows, rows_per_block);
@@ -223,7 +234,7 @@ void k_score_topk(
     for (int i = tid; i < nr; i += kFzBS) {
       const int32_t unit = rows_unit[r0 + i];
       su[i] = unit;
-      sq[i][D + 2] = sp.tie_rotated ? salt[unit] : 0u;
+      sq[i][SALT] = sp.tie_rotated ? salt[unit] : 0u;
     }
   } else {
     for (int i = tid; i < nr * SQW; i += kFzBS) {
@@ -309,17 +320,34 @@ void k_score_topk(
   static_assert(!PRE || kFzRC * Q4 <= 64, "one record piece per lane");
   const int cls = PRE ? tcls[(tile0 >> 7) + wave] : 0;
   const uint4 *crec4 = reinterpret_cast<const uint4 *>(crec);
+#if KP_FZ_DMA
+  // rows c .. c + kFzRC - 1 into srec[b][wave]: lane l copies 16-B piece l % Q4
+  // of row l / Q4 to byte 16·l of the buffer (the LDS DMA's lane layout)
+  auto rec_dma = [&](int c, int b) {
+    if (lane < min(kFzRC, nr - c) * Q4)
+      __builtin_amdgcn_global_load_lds(crec4 + ((int64_t)su[c + lane / Q4] * nfc + cls) * Q4 + lane % Q4,
+                                       (void __attribute__((address_space(3))) *)&srec[b][wave][0][0], 16, 0, 0);
+  };
+  if (PRE) rec_dma(0, 0);
+#else
   uint4 nx = make_uint4(0u, 0u, 0u, 0u);
   if (PRE && lane < min(kFzRC, nr) * Q4)
     nx = crec4[((int64_t)su[lane / Q4] * nfc + cls) * Q4 + lane % Q4];
+#endif
   for (int c0 = 0; c0 < nr; c0 += kFzRC) {
     const int cr = min(kFzRC, nr - c0);
     const int buf = NB == 2 ? (c0 / kFzRC) & 1 : 0;
+    const int rb = NRB == 2 ? (c0 / kFzRC) & 1 : 0;
     if constexpr (PRE) {  // 1a. the chunk's row records: one 16-B piece per lane
-      if (lane < cr * Q4) reinterpret_cast<uint4 *>(srec[wave][lane / Q4])[lane % Q4] = nx;
+#if KP_FZ_DMA
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this chunk's copy has landed
+      if (c0 + kFzRC < nr) rec_dma(c0 + kFzRC, rb ^ 1);
+#else
+      if (lane < cr * Q4) reinterpret_cast<uint4 *>(srec[0][wave][lane / Q4])[lane % Q4] = nx;
       const int c1 = c0 + kFzRC;
       if (lane < min(kFzRC, nr - c1) * Q4)
         nx = crec4[((int64_t)su[c1 + lane / Q4] * nfc + cls) * Q4 + lane % Q4];
+#endif
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -330,7 +358,7 @@ void k_score_topk(
 #pragma unroll
     for (int rb = 0; rb < kFzRC; rb += RPI) {
       const int rr = rb + lane / DP, d = lane % DP;
-      uint32_t *rec = srec[wave][rr];
+      uint32_t *rec = srec[0][wave][rr];
       uint32_t tthr = 0xFFFFFFFFu, twq = 0, tok = 1u;
       if (rr < cr && d < D) {
         const uint32_t qd = sq[c0 + rr][d];
@@ -399,7 +427,7 @@ void k_score_topk(
 #endif
       for (int i = 0; i < cr; ++i) {
         RowRec<RW> cur;
-        cur.load(srec[wave][i]);
+        cur.load(srec[rb][wave][i]);
         const uint32_t wq = cur[2 * D + 2], qg = cur[D], af = cur[D + 1];
         const int32_t wfr = (int32_t)cur[2 * D + 3];
         // the row's terms, wave-uniform: a request no column of the wave's
@@ -469,7 +497,7 @@ void k_score_topk(
     if (wave < cr) {
       const int i = wave;
       const int64_t row = r0 + c0 + i;
-      const uint32_t nsl = ~sq[c0 + i][D + 2];
+      const uint32_t nsl = ~sq[c0 + i][SALT];
       // select-phase tie bits: (nst - tsp[g] - j * mt) >> rsh
       const uint32_t *tsp = tie0 ? spos0 : spos;
       const uint32_t nst = tie0 ? (spos[0] + (uint32_t)(kFzTile - 1)) << (32 - TB) : nsl,
@@ -579,27 +607,31 @@ void k_score_topk(
       uint64_t *dst = part + (row * ntiles + tile) * K;
       if (C <= 64) {
         const uint64_t my = lane < C ? sbuf[wave][lane] : 0ull;
-        const uint32_t mlo = (uint32_t)my, mhi = (uint32_t)(my >> 32);
         int r = 0;
-        for (int j = 0; j < C; ++j) {
-          const uint64_t o = ((uint64_t)rl(mhi, j) << 32) | rl(mlo, j);
-          r += o > my ? 1 : 0;
+        // the other keys as LDS broadcast reads, two per 16-B read (a
+        // v_readlane pair per key cost config #4 +25 ms)
+        const ulonglong2 *sb2 = reinterpret_cast<const ulonglong2 *>(sbuf[wave]);
+#pragma unroll KP_FZ_RANK_UNROLL
+        for (int j = 0; j < C / 2; ++j) {
+          const ulonglong2 o = sb2[j];
+          r += (o.x > my ? 1 : 0) + (o.y > my ? 1 : 0);
         }
+        if (C & 1) r += sbuf[wave][C - 1] > my ? 1 : 0;
         if (lane < C && r < K) dst[r] = my;
         if (lane >= C && lane < K) dst[lane] = 0ull;
       } else {  // 64 < C <= 128 (K <= 64 < C: every slot is filled)
         const uint64_t my0 = sbuf[wave][lane];
         const uint64_t my1 = lane + 64 < C ? sbuf[wave][lane + 64] : 0ull;
-        const uint32_t alo = (uint32_t)my0, ahi = (uint32_t)(my0 >> 32);
-        const uint32_t blo = (uint32_t)my1, bhi = (uint32_t)(my1 >> 32);
+        const ulonglong2 *sb2 = reinterpret_cast<const ulonglong2 *>(sbuf[wave]);
         int r0 = 0, r1 = 0;
-        for (int j = 0; j < 64; ++j) {
-          const uint64_t o = ((uint64_t)rl(ahi, j) << 32) | rl(alo, j);
-          r0 += o > my0 ? 1 : 0;
-          r1 += o > my1 ? 1 : 0;
+#pragma unroll KP_FZ_RANK_UNROLL
+        for (int j = 0; j < C / 2; ++j) {
+          const ulonglong2 o = sb2[j];
+          r0 += (o.x > my0 ? 1 : 0) + (o.y > my0 ? 1 : 0);
+          r1 += (o.x > my1 ? 1 : 0) + (o.y > my1 ? 1 : 0);
         }
-        for (int j = 64; j < C; ++j) {
-          const uint64_t o = ((uint64_t)rl(bhi, j - 64) << 32) | rl(blo, j - 64);
+        if (C & 1) {
+          const uint64_t o = sbuf[wave][C - 1];
           r0 += o > my0 ? 1 : 0;
           r1 += o > my1 ? 1 : 0;
         }
