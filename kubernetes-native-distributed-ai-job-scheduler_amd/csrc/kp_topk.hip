@@ -62,8 +62,11 @@
 #ifndef KP_FZ_DMA
 #define KP_FZ_DMA 1  // PRE row records by LDS DMA (0: through VGPRs; A/B knob)
 #endif
+#ifndef KP_FZ_GSURV
+#define KP_FZ_GSURV 1  // survivor scan over the groups whose best reached T (0: the lanes)
+#endif
 #ifndef KP_FZ_RANK_UNROLL
-#define KP_FZ_RANK_UNROLL 4  // survivor rank loop unroll (A/B knob)
+#define KP_FZ_RANK_UNROLL 2  // survivor rank loop unroll (4: +10 ms on config #4, spills)
 #endif
 #ifndef KP_FZ_ROW_UNROLL
 #define KP_FZ_ROW_UNROLL 1  // rows of the score loop interleaved (A/B knob)
@@ -205,7 +208,7 @@ void k_score_topk(
   __shared__ __attribute__((aligned(16))) uint64_t sbuf[NW][kFzSurv];
   __shared__ uint32_t spos[NG + NG / 64];   // per group (padded like the tile rows)
   __shared__ uint32_t spos0[NG + NG / 64];  // tie mode 0: the select-phase tie bits
-  __shared__ uint8_t scand[NW][64];  // per wave: lanes whose best reached T
+  __shared__ uint8_t scand[NW][KP_FZ_GSURV ? 64 * GPL : 64];  // per wave: lanes / groups whose best reached T
   constexpr int RW = (2 * D + 4 + 3) & ~3;  // row record words, whole 16-B reads
   // PRE + KP_FZ_DMA: two buffers, the next chunk's records copied by the
   // memory unit straight into LDS while the current chunk is scored
@@ -502,23 +505,31 @@ void k_score_topk(
       const uint32_t *tsp = tie0 ? spos0 : spos;
       const uint32_t nst = tie0 ? (spos[0] + (uint32_t)(kFzTile - 1)) << (32 - TB) : nsl,
                      mt = tie0 ? 1u << (32 - TB) : mul;
-      // lane L's 16 columns are the 4 groups 4L .. 4L + 3 (contiguous, so the
-      // survivor scan below reads one candidate lane's columns from 16
-      // consecutive LDS entries), visited in an order rotated by lane / 8
-      // (lane / 4 for 16-B groups): the lanes of one LDS access then cover
-      // every bank once (a plain 4L + k order would be 4-way conflicted)
+      // lane L's 16 columns are the 4-column groups L + 64k, k < GPL
+      // (strided: the tile's best keys spread over the lanes; the padded rows
+      // keep both this pass and the survivor scan free of bank conflicts)
       uint32_t best = 0;
+#if KP_FZ_GSURV
+      uint32_t gb[GPL];  // the lane's best key per group
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
       for (int k = 0; k < GPL; ++k) {
         uint32_t v4[4];
-        const int gk = pgi(lane + 64 * k);  // lane L: groups L + 64k (strided: the
-        load_group<H16>(ssc[buf][i], gk, v4);  // tile's best keys spread over the lanes)
+        const int gk = pgi(lane + 64 * k);
+        load_group<H16>(ssc[buf][i], gk, v4);
         const uint32_t npk = nst - tsp[gk];
+        uint32_t b4 = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const uint32_t s1 = v4[j];
-          best = max(best, (s1 << ksh) | ((npk - (uint32_t)j * mt) >> rsh));
+          b4 = max(b4, (s1 << ksh) | ((npk - (uint32_t)j * mt) >> rsh));
         }
+        best = max(best, b4);
+#if KP_FZ_GSURV
+        gb[k] = b4;
+#endif
       }
       // T = the K-th largest lane best (radix select over ballots; lower
       // bound of the tile's K-th key), at least 1 << ksh: every key >= T is
@@ -531,29 +542,53 @@ void k_score_topk(
         T = __popcll(__ballot(best >= cb)) >= K ? cb : T;
       }
       T = max(T, 1u << ksh);
+      KP_FZ_PROF_MARK(6);
+#if KP_FZ_GSURV
+      // survivors (keys >= T) -> LDS as exact 64-bit keys. Only the groups
+      // whose best reached T hold any (at least K of them, typically about
+      // K): their (lane, k) go to LDS in order and the whole wave scans just
+      // their 4 columns each (a lane-granular list scanned 16 columns per
+      // listed lane, 4x the work)
+      int m = 0;
+#pragma unroll
+      for (int k = 0; k < GPL; ++k) {
+        const uint64_t Mk = __ballot(gb[k] >= T);
+        if (gb[k] >= T)
+          scand[wave][m + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(Mk >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)Mk, 0u))] =
+              (uint8_t)(lane | (k << 6));
+        m += __popcll(Mk);
+      }
+      constexpr int CPL = 4;  // columns per listed entry
+#else
       // survivors (keys >= T) -> LDS as exact 64-bit keys. Only lanes whose
       // best reached T hold any (at least K of them): their lane numbers go
       // to LDS in order and the whole wave scans just their 16 columns each
-      KP_FZ_PROF_MARK(6);
       const uint64_t M = __ballot(best >= T);
       const int m = __popcll(M);
       if (best >= T)
         scand[wave][__builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
                                               __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u))] =
             (uint8_t)lane;
+      constexpr int CPL = 4 * GPL;  // columns per lane
+#endif
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       const uint32_t *srow = ssc[buf][i];
       int C = 0;
-      constexpr int CPL = 4 * GPL;  // columns per lane
       for (int e0 = 0; e0 < CPL * m; e0 += 64) {  // wave-uniform
         const int e = e0 + lane;
         bool hit = false;
         uint32_t s1 = 0, ntk = 0;
         if (e < CPL * m) {
+#if KP_FZ_GSURV
+          const int ent = scand[wave][e >> 2];  // listed (lane, group k)
+          const int g = pgi((ent & 63) + 64 * (ent >> 6)), jj = e & 3;
+#else
           const int L = scand[wave][e / CPL];          // candidate lane
           const int g = pgi(L + 64 * ((e >> 2) & (GPL - 1))), jj = e & 3;  // its column group, column
+#endif
           s1 = load_one<H16>(srow, 4 * g + jj);
           ntk = nsl - spos[g] - (uint32_t)jj * mul;
           hit = ((s1 << ksh) | ((nst - tsp[g] - (uint32_t)jj * mt) >> rsh)) >= T;
