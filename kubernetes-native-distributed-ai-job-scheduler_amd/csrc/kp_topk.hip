@@ -65,6 +65,9 @@
 #ifndef KP_FZ_GSURV
 #define KP_FZ_GSURV 1  // survivor scan over the groups whose best reached T (0: the lanes)
 #endif
+#ifndef KP_FZ_FEWSKIP
+#define KP_FZ_FEWSKIP 1  // skip the radix search when fewer than K lane bests are feasible
+#endif
 #ifndef KP_FZ_RANK_UNROLL
 #define KP_FZ_RANK_UNROLL 2  // survivor rank loop unroll (4: +10 ms on config #4, spills)
 #endif
@@ -536,6 +539,11 @@ void k_score_topk(
       // feasible
       KP_FZ_PROF_MARK(5);
       uint32_t T = 0;
+#if KP_FZ_FEWSKIP
+      // fewer than K lanes with a feasible best: the K-th lane best is below
+      // 1 << ksh and T is 1 << ksh without the search (wave-uniform)
+      if (__popcll(__ballot(best >= (1u << ksh))) >= K)
+#endif
 #pragma unroll
       for (int bb = 31; bb >= 0; --bb) {
         const uint32_t cb = T | (1u << bb);

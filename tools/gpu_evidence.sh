@@ -41,10 +41,10 @@ pmc WRITE_SIZE WRITE_SIZE || exit $?
 pmc SQ1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY || exit $?
 pmc LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVES || exit $?
 # the same SQ pass on a k_score_topk build without its select phase
-# (tools/build_variant.sh WORKTREE noselect -DKP_FZ_EXP=1): score + threshold
+# (ABOUT=$PWD/abl tools/build_variant.sh WORKTREE noselect -DKP_FZ_EXP=1): score + threshold
 # stages alone; the select phase is the difference (its round 0 only: no
 # candidates, the solve ends after one round)
-NOSEL=kubernetes-native-distributed-ai-job-scheduler_amd/build/ab/noselect.so
+NOSEL=${NOSEL:-abl/noselect.so}
 if [ -f $NOSEL ]; then
   export KPLACE_LIB=$PWD/$NOSEL
   pmc SQ_NOSEL SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY || exit $?
