@@ -290,10 +290,12 @@ def config4(args, make_placer, n_gpus=1, barrier=lambda: None, max_over_ranks=la
             if it:  # first iteration: warmup
                 sol.append(max_over_ranks(t1 - t0))
                 pre.append(max_over_ranks(t2 - t1b))
-        progress("config #4 phase split")
-        phases = phase_split(pl, p, gather=gather)
-        pl.reset_nodes()
-        phases["preempt_ms"] = 1e3 * float(np.mean(pre))
+        phases = None
+        if not args.no_phases:
+            progress("config #4 phase split")
+            phases = phase_split(pl, p, gather=gather)
+            pl.reset_nodes()
+            phases["preempt_ms"] = 1e3 * float(np.mean(pre))
     s_ms, p_ms = 1e3 * float(np.mean(sol)), 1e3 * float(np.mean(pre))
     util = w.used.sum(1) / w.cap.sum(1)
     cpu = None if args.no_cpu_baseline or n_gpus > 1 else config4_cpu(args, w, p)
@@ -418,6 +420,9 @@ def main():
                     help="config #4 CPU baseline sample: rounds of their solve")
     ap.add_argument("--cpu-stream-batches", type=int, default=4,
                     help="config #5 CPU baseline sample: the first N micro-batches")
+    ap.add_argument("--no-phases", action="store_true",
+                    help="skip the extra solve with per-round phase events (profiling runs that count "
+                         "kernel launches per solve)")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="time the steps without per-launch HIP events (no roofline)")
     args = ap.parse_args()
@@ -530,7 +535,7 @@ def main():
     # where a solve's time goes (outside the timed steps): candidate phase /
     # exchange / passes, max over ranks
     progress("phase split")
-    phases = phase_split(pl, p, gather=gather)
+    phases = None if args.no_phases else phase_split(pl, p, gather=gather)
 
     # full-queue placement latency: snapshot in host memory -> assignment in
     # host memory (kp_place: validate + H2D + solve + D2H), outside the steps

@@ -1665,16 +1665,25 @@ int kp_score_dev(kp_ctx *c, const kp_params *p, int32_t job_lo, int32_t job_hi,
   const int64_t chunk = (int64_t)65535 * 64;
   for (int64_t r0 = 0; r0 < rows; r0 += chunk) {
     const int32_t nr = (int32_t)std::min<int64_t>(chunk, rows - r0);
+    // profiling: the kernel's own start / end stamps (hipExtLaunchKernel),
+    // not events recorded around the launch call, which also caught the
+    // device idling while the host submitted the kernel (~80 us per call)
+    // (the class form; the other forms keep events around the launch)
+    const bool ext = tm.score_form == 1;
     hipEvent_t a = nullptr, b = nullptr;
     if (c->profiling) {
-      KP_TRY(E.make(&a, hipEventDisableSystemFence));
-      KP_TRY(E.make(&b, hipEventDisableSystemFence));
-      KP_HIP(hipEventRecord(a, c->stream));
+      KP_TRY(E.make(&a, 0));
+      KP_TRY(E.make(&b, 0));
+      if (!ext) KP_HIP(hipEventRecord(a, c->stream));
     }
-    KP_TRY(launch_score(c, sp, c->d.rowmap + r0, nr, score_dev ? score_dev + r0 * Ns : nullptr,
-                        mask_dev ? mask_dev + r0 * words : nullptr, c->d.q, c->U));
+    c->score_ev0 = ext ? a : nullptr;
+    c->score_ev1 = ext ? b : nullptr;
+    const int rc = launch_score(c, sp, c->d.rowmap + r0, nr, score_dev ? score_dev + r0 * Ns : nullptr,
+                                mask_dev ? mask_dev + r0 * words : nullptr, c->d.q, c->U);
+    c->score_ev0 = c->score_ev1 = nullptr;
+    KP_TRY(rc);
     if (c->profiling) {
-      KP_HIP(hipEventRecord(b, c->stream));
+      if (!ext) KP_HIP(hipEventRecord(b, c->stream));
       KP_HIP(hipEventSynchronize(b));
       c->timing.score_ms += ev_ms(a, b);
     }

@@ -209,6 +209,9 @@ struct kp_ctx {
   int64_t max_pairs_matrix = 0;
   hipStream_t stream = nullptr;
   int profiling = 0;  // kp_set_profiling level (0 off, 1 filter+score events, 2 + phase split)
+  // kp_score_dev under profiling: the events hipExtLaunchKernel stamps at the
+  // start and end of the next k_score32c launch (kernel time only)
+  hipEvent_t score_ev0 = nullptr, score_ev1 = nullptr;
   hipEvent_t fz_end_event = nullptr;  // profiling: recorded right after k_score_topk
   // test knobs, read from the environment at kp_create (never set in
   // production): KP_SELECT_LDS_CAP shrinks the threshold select's survivor

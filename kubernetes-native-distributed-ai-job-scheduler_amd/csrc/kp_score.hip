@@ -6,6 +6,7 @@
 // streaming (score matrix stores, row re-reads), keeping the node tile in
 // VGPRs across job rows, and 64-lane wave ballots / shuffles for the masks,
 // argmax and prefix sums.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1319,7 +1320,8 @@ struct ScoreL {
             (int)std::min<int64_t>(kScoreClsRows, std::max<int64_t>(c->score_min_rpb, want));
         const dim3 grid(ctiles, blocks(rows, rpb));
 #define KP_SC32C(M, WS_, WM_)                                                                  \
-  hipLaunchKernelGGL((k_score32c<D, M, WS_, WM_>), grid, dim3(256), 0, c->stream, sp, c->d.np32, P, \
+  hipExtLaunchKernelGGL((k_score32c<D, M, WS_, WM_>), grid, dim3(256), 0, c->stream, c->score_ev0,   \
+                        c->score_ev1, 0, sp, c->d.np32, P,                                         \
                      q, qstride, c->d.aff, rows_unit, rows, rpb, c->score_min_rpb, score,           \
                      sstride > 0 ? sstride : (int64_t)Ns, mask, mstride > 0 ? mstride : (int64_t)Ns / 64, \
                      Ns, rows_dev, c->d.ccap, c->n_classes)

@@ -497,7 +497,11 @@ void k_score_topk(
     //    bits of ~tk, ~tk = ~(pos*mul + salt) = ~salt - pos*mul
 #if KP_FZ_EXP == 1  // timing experiment: no select phase
     if (wave < cr && lane < K)  // no candidates (keeps the merge in bounds)
-      part[((r0 + c0 + wave) * ntiles + tile) * K + lane] = (uint64_t)(ssc[0][wave][lane] & 0);
+      // (0 at run time: n_cand < 2^16; an opaque mask keeps the LDS tile's
+      // stores alive — with a literal & 0 the compiler dropped them and the
+      // whole score stage with them)
+      part[((r0 + c0 + wave) * ntiles + tile) * K + lane] =
+          (uint64_t)(ssc[buf][wave][lane] & (uint32_t)(sp.n_cand >> 16));
     if (false)
 #endif
     if (wave < cr) {
