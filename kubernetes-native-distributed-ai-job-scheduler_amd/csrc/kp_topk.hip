@@ -72,7 +72,7 @@
 #define KP_FZ_RANK_UNROLL 2  // survivor rank loop unroll (4: +10 ms on config #4, spills)
 #endif
 #ifndef KP_FZ_ROW_UNROLL
-#define KP_FZ_ROW_UNROLL 1  // rows of the score loop interleaved (A/B knob)
+#define KP_FZ_ROW_UNROLL 2  // rows of the score loop interleaved (1: config #4 +2 ms, r05)
 #endif
 
 namespace kp {
