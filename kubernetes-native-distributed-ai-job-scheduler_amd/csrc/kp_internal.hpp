@@ -231,7 +231,7 @@ struct kp_ctx {
   int32_t acc_waves = 2048;
   int32_t acc_list = 1;  // KP_ACC_LIST=0: k_accept walks every node while entries >= nodes
   // KP_COMPACT_MAX: largest unit range compacted by the one-workgroup kernel
-  int32_t compact_max = 262144;
+  int32_t compact_max = 65536;
   bool preempt32 = true;  // KP_PREEMPT32=0: the 64-bit per-row preemption kernel on 32-bit tables too
   // the victim pool's (victims, priority sum, node) fits one ordered 64-bit
   // key (N < 2^20, < 2^11 running jobs per node, |sum of their priorities| < 2^31)

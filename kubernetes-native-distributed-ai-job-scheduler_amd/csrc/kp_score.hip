@@ -1501,7 +1501,7 @@ static int launch_round_start(kp_ctx *c, int32_t lo, int32_t hi, int32_t *flag) 
 int launch_pack(kp_ctx *c) { return launch_round_start(c, 0, 0, nullptr); }
 
 // flags[0, n) -> out (lo + index, rank order; act_local by default), count ->
-// counters[0]; one workgroup up to KP_COMPACT_MAX flags (default 262,144),
+// counters[0]; one workgroup up to KP_COMPACT_MAX flags (default 65,536),
 // the two-launch multi-workgroup form above (chunk counts in `temp`)
 int launch_compact_to(kp_ctx *c, const int32_t *flag, int32_t lo, int32_t n, int32_t *out,
                       int32_t *host_count) {
