@@ -59,6 +59,12 @@
 #define KP_ACC_WPB 1  // k_accept waves per workgroup (1 vs 4: -0.2 ms per config #3 solve)
 #endif
 static_assert(KP_ACC_WPB >= 1 && KP_ACC_WPB <= 16, "node records carry 16 spare entries");
+#ifndef KP_CSR_PLACE_T
+#define KP_CSR_PLACE_T 1  // k_csr_place_t (candidate-major entry writes); 0: one thread per candidate
+#endif
+#ifndef KP_CSR_PLACE_T_MIN
+#define KP_CSR_PLACE_T_MIN (1 << 20)  // bidder entries from which k_csr_place_t is used
+#endif
 #ifndef KP_ROWS_WPB
 #define KP_ROWS_WPB 16  // k_csr_rows rows (waves) per workgroup
 #endif
@@ -407,6 +413,58 @@ __global__ void k_csr_place(int32_t A, int32_t K, int32_t D, int32_t U, int64_t 
   ent_size[e] = size[u];
   ent_lead[e] = leader[u];
   for (int d = 0; d < D; ++d) ent_q[(int64_t)d * P + e] = q[(int64_t)d * U + u];
+}
+
+// The same placement in two phases per 1,024-thread workgroup of S = 1024 / K
+// slots: entry indices computed slot-major (coalesced candidate reads and
+// inverse-index writes), then the entry operands written candidate-major —
+// the lanes of one candidate index over consecutive slots, which in herded
+// rounds (consecutive slots bidding the same node) land on consecutive
+// entries of one bidder row: whole-line stores instead of 16-B pieces.
+__global__ __launch_bounds__(1024) void k_csr_place_t(
+    int32_t A, int32_t K, int32_t D, int32_t U, int64_t Wb, int64_t P, const int32_t *__restrict__ A_dev,
+    const int32_t *__restrict__ cand, const int32_t *__restrict__ act, const int64_t *__restrict__ q,
+    const int32_t *__restrict__ size, const int32_t *__restrict__ leader,
+    const int32_t *__restrict__ seg_start, const int32_t *__restrict__ cnt, int32_t bmin_windows,
+    const uint2 *__restrict__ rowinfo, int32_t *__restrict__ inv, int32_t *__restrict__ ent_unit,
+    int32_t *__restrict__ ent_slot, int32_t *__restrict__ ent_size, int32_t *__restrict__ ent_lead,
+    int64_t *__restrict__ ent_q) {
+  __shared__ int32_t se[2048];  // entry of (slot al, candidate j) at al * (K + 1) + j (conflict-free)
+  const int32_t Aa = A_dev ? min(A, *A_dev) : A;
+  const int S = 1024 / K, tl = threadIdx.x;
+  const int64_t a0 = (int64_t)blockIdx.x * S;
+  if (a0 >= Aa) return;  // workgroup-uniform
+  if (tl < S * K) {
+    const int32_t al = tl / K, j = tl - al * K;
+    const int64_t a = a0 + al;
+    int32_t e = -1;
+    if (a < Aa) {
+      const int64_t t = a * K + j;
+      const int32_t n = cand[t];
+      if (n >= 0) {
+        const int32_t ss = seg_start[n], len = cnt[n];
+        const uint2 ri = rowinfo[(int64_t)n * Wb + (a >> 5)];
+        e = ss + (int32_t)ri.x + __popc(ri.y & ((1u << (a & 31)) - 1u));
+        const bool lrow = ((ss + len - 1) >> 6) - (ss >> 6) + 1 >= bmin_windows;
+        inv[t] = e | (lrow ? (int32_t)0x80000000u : 0);
+      }
+    }
+    se[al * (K + 1) + j] = e;
+  }
+  __syncthreads();
+  if (tl < S * K) {
+    const int32_t j = tl / S, al = tl - j * S;
+    const int64_t a = a0 + al;
+    const int32_t e = se[al * (K + 1) + j];
+    if (a < Aa && e >= 0) {
+      const int32_t u = act[a];
+      ent_unit[e] = u;
+      ent_slot[e] = (int32_t)a;
+      ent_size[e] = size[u];
+      ent_lead[e] = leader[u];
+      for (int d = 0; d < D; ++d) ent_q[(int64_t)d * P + e] = q[(int64_t)d * U + u];
+    }
+  }
 }
 
 // ---- plan ------------------------------------------------------------------------
@@ -1451,6 +1509,16 @@ int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev) {
                        c->d.counters + 32, c->d.counters + 33);
     KP_HIP(hipGetLastError());
     c->bm_dirty = false;
+#if KP_CSR_PLACE_T
+    // large rounds only (config #4: -3 ms per solve); below ~1M entries the
+    // one-pass form is faster (config #3 +0.2 ms with the two-phase form)
+    if (K <= 1024 && P >= (int64_t)KP_CSR_PLACE_T_MIN) {
+      hipLaunchKernelGGL(k_csr_place_t, dim3(blocks(A, 1024 / K)), dim3(1024), 0, c->stream, A, K, c->D,
+                         c->U, Wb, P, A_dev, c->d.cand, c->d.act, c->d.q, c->d.size, c->d.leader,
+                         c->d.seg_start, c->d.cnt, c->bmin_windows, c->d.rowinfo, c->d.inv,
+                         c->d.ent_unit, c->d.ent_slot, c->d.ent_size, c->d.ent_lead, c->d.ent_q);
+    } else
+#endif
     hipLaunchKernelGGL(k_csr_place, dim3(blocks(P, 256)), dim3(256), 0, c->stream, A, K, c->D,
                        c->U, Wb, P, A_dev, c->d.cand, c->d.act, c->d.q, c->d.size, c->d.leader,
                        c->d.seg_start, c->d.cnt, c->bmin_windows, c->d.rowinfo, c->d.inv,
