@@ -83,6 +83,10 @@ using namespace dev;
 #define KP_MERGE_WPB 4  // k_merge_tour rows (waves) per workgroup
 #endif
 constexpr int kMergeWPB = KP_MERGE_WPB;
+#ifndef KP_MERGE_LOAD_BATCH
+#define KP_MERGE_LOAD_BATCH 8  // k_merge_tour: list loads per lane in flight (1: one 64-key load at a time)
+#endif
+constexpr int kMergeLoadBatch = KP_MERGE_LOAD_BATCH;
 constexpr int kFzMaxRows = 128;          // rows per workgroup (request stage)
 constexpr int kFzSurv = 128;             // survivor slots per wave (2 per lane)
 // Workgroup shape of k_score_topk: NW waves x 128 columns (2 per lane) =
@@ -758,7 +762,21 @@ __global__ __launch_bounds__(64 * KP_MERGE_WPB) void k_merge_tour(ScoreParams sp
   const int K = sp.n_cand, M = ntiles * K;
   uint64_t *L = slist + (int64_t)wave * M;
   const uint64_t *src = part + (int64_t)row * M;
-  for (int e = lane; e < M; e += 64) L[e] = src[e];
+  // the row's lists staged in batches of 8 loads per lane issued together (a
+  // load-then-store loop waited one memory latency per 64 keys)
+  for (int b0 = 0; b0 < M; b0 += 64 * kMergeLoadBatch) {
+    uint64_t x[kMergeLoadBatch];
+#pragma unroll
+    for (int u = 0; u < kMergeLoadBatch; ++u) {
+      const int e = b0 + 64 * u + lane;
+      x[u] = e < M ? src[e] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < kMergeLoadBatch; ++u) {
+      const int e = b0 + 64 * u + lane;
+      if (e < M) L[e] = x[u];
+    }
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
