@@ -83,6 +83,9 @@ using namespace dev;
 #define KP_MERGE_WPB 4  // k_merge_tour rows (waves) per workgroup
 #endif
 constexpr int kMergeWPB = KP_MERGE_WPB;
+#ifndef KP_MERGE_KEYS_COMBINE
+#define KP_MERGE_KEYS_COMBINE 1  // one bitmap atomic per (node, candidate index) per merge workgroup
+#endif
 #ifndef KP_MERGE_LOAD_BATCH
 #define KP_MERGE_LOAD_BATCH 8  // k_merge_tour: list loads per lane in flight (1: one 64-key load at a time)
 #endif
@@ -758,36 +761,77 @@ __global__ __launch_bounds__(64 * KP_MERGE_WPB) void k_merge_tour(ScoreParams sp
     return;
   }
   const int row = blockIdx.x * kMergeWPB + wave;
-  if (row >= rows || (rows_dev && row >= *rows_dev)) return;  // wave-uniform, no barrier below
+  const bool live = row < rows && !(rows_dev && row >= *rows_dev);  // wave-uniform
+#if !KP_MERGE_KEYS_COMBINE
+  if (!live) return;  // no barrier below
+#endif
   const int K = sp.n_cand, M = ntiles * K;
-  uint64_t *L = slist + (int64_t)wave * M;
-  const uint64_t *src = part + (int64_t)row * M;
-  // the row's lists staged in batches of 8 loads per lane issued together (a
-  // load-then-store loop waited one memory latency per 64 keys)
-  for (int b0 = 0; b0 < M; b0 += 64 * kMergeLoadBatch) {
-    uint64_t x[kMergeLoadBatch];
+  int32_t unit = 0, mine = -1;
+  if (live) {
+    uint64_t *L = slist + (int64_t)wave * M;
+    const uint64_t *src = part + (int64_t)row * M;
+    // the row's lists staged in batches of 8 loads per lane issued together (a
+    // load-then-store loop waited one memory latency per 64 keys)
+    for (int b0 = 0; b0 < M; b0 += 64 * kMergeLoadBatch) {
+      uint64_t x[kMergeLoadBatch];
 #pragma unroll
-    for (int u = 0; u < kMergeLoadBatch; ++u) {
-      const int e = b0 + 64 * u + lane;
-      x[u] = e < M ? src[e] : 0ull;
+      for (int u = 0; u < kMergeLoadBatch; ++u) {
+        const int e = b0 + 64 * u + lane;
+        x[u] = e < M ? src[e] : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < kMergeLoadBatch; ++u) {
+        const int e = b0 + 64 * u + lane;
+        if (e < M) L[e] = x[u];
+      }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    unit = rows_unit[row];
+    const uint32_t sl = sp.tie_rotated ? salt[unit] : 0u;
+    const uint32_t inv = sp.tie_rotated ? kTieMulInv : 1u;
+    const int32_t mypos = merge_tour_row<LPL>(L, ntiles, K, sl, inv, lane);
+    // canonical position -> node (a position is always < N)
+    mine = (uint32_t)mypos < (uint32_t)sp.N ? perm[mypos] : -1;
+    if (lane < K) cand[(int64_t)row * K + lane] = mine;
+  }
+#if KP_MERGE_KEYS_COMBINE
+  if (rk.enabled) {  // k_csr_keys' work for the workgroup's slots
+    // the slots of a workgroup share one bitmap word (kMergeWPB divides 32):
+    // the first wave with node n at candidate index j sets the bits of every
+    // wave with n at j in one atomic (herded rounds: consecutive slots list
+    // the same nodes in the same order)
+    static_assert(32 % kMergeWPB == 0, "a workgroup's slots in one bitmap word");
+    __shared__ int32_t snode[kMergeWPB][64];
+    snode[wave][lane] = live ? mine : -1;
+    __syncthreads();
+    if (live) {
+      if (lane < K) {
+        rk.bid[(int64_t)row * K + lane] = 0xFFFFFFFFu;  // kNoBid
+        if (mine >= 0) {
+          bool first = true;
+          uint32_t bits = 0;
 #pragma unroll
-    for (int u = 0; u < kMergeLoadBatch; ++u) {
-      const int e = b0 + 64 * u + lane;
-      if (e < M) L[e] = x[u];
+          for (int w2 = 0; w2 < kMergeWPB; ++w2)
+            if (snode[w2][lane] == mine) {
+              first = first && w2 >= wave;
+              bits |= 1u << ((blockIdx.x * kMergeWPB + w2) & 31);
+            }
+          if (first && atomicOr(&rk.bm[(int64_t)mine * rk.Wb + (row >> 5)], bits) == 0u)
+            atomicOr(&rk.bms[(int64_t)mine * rk.Ws + (row >> 10)], 1u << ((row >> 5) & 31));
+        }
+      }
+      const int32_t first_node = __shfl(mine, 0, 64);
+      if (lane == 0) {
+        rk.open[row] = first_node >= 0 ? 1 : 0;
+        if (first_node < 0) rk.status[unit] = kNoFit;
+      }
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int32_t unit = rows_unit[row];
-  const uint32_t sl = sp.tie_rotated ? salt[unit] : 0u;
-  const uint32_t inv = sp.tie_rotated ? kTieMulInv : 1u;
-  const int32_t mypos = merge_tour_row<LPL>(L, ntiles, K, sl, inv, lane);
-  // canonical position -> node (a position is always < N)
-  const int32_t mine = (uint32_t)mypos < (uint32_t)sp.N ? perm[mypos] : -1;
-  if (lane < K) cand[(int64_t)row * K + lane] = mine;
+#else
   if (rk.enabled) round_keys_slot(rk, row, unit, K, mine, lane);  // k_csr_keys' work for the slot
+#endif
 }
 
 template <int D>
