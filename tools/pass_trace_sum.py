@@ -10,7 +10,7 @@ rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Time
 starts = [i for i, r in enumerate(rows) if "k_reset_units" in r["Kernel_Name"]]
 seq = rows[starts[-1]:]
 dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-rb = [i for i, r in enumerate(seq) if "k_round_begin" in r["Kernel_Name"]]
+rb = [i for i, r in enumerate(seq) if "k_round_begin" in r["Kernel_Name"] or "k_round_start" in r["Kernel_Name"]]
 acc_p, plan_p = defaultdict(list), defaultdict(list)
 per_round = []
 for ri, a in enumerate(rb):
