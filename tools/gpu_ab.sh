@@ -3,8 +3,8 @@
 # libkplace.so): config #3 solve (tools/cfg_time.py) alternated x3, then the
 # config #4 solve (tools/c4_time.py) alternated x2. LIBS overrides the list.
 set -o pipefail
-OUT=gpurun_out/r05ab; mkdir -p $OUT
-LIBS=${LIBS:-"r04 c1 cur"}
+OUT=gpurun_out/ab_libs; mkdir -p $OUT
+LIBS=${LIBS:-"base cur"}
 lib_of() { [ "$1" = cur ] && echo "$PWD/kubernetes-native-distributed-ai-job-scheduler_amd/libkplace.so" || echo "$PWD/abl/$1.so"; }
 for i in 1 2 3; do for l in $LIBS; do
   KPLACE_LIB=$(lib_of $l) timeout -k 10 120 python3 tools/cfg_time.py >> $OUT/c3.txt 2>&1 || { tail -5 $OUT/c3.txt; exit 1; }

@@ -1,19 +1,19 @@
-# r05: config #4 per-kernel time and k_score_topk's VALU lane-ops per pair
+# Config #4 per-kernel time and k_score_topk's VALU lane-ops per pair
 # (tools/c4_time.py: 3 solves; summarised per solve into $OUT/summary.txt)
 set -o pipefail
-OUT=gpurun_out/r05c4p; rm -rf $OUT; mkdir -p $OUT
+OUT=gpurun_out/c4_profile; rm -rf $OUT; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ks -o run -- python3 tools/c4_time.py > $OUT/ks.log 2>&1 || exit $?
 rm -f $OUT/ks/run_kernel_trace.csv
 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY --kernel-include-regex k_score_topk --output-format csv -d $OUT/sq -o run -- python3 tools/c4_time.py > $OUT/sq.log 2>&1 || exit $?
 python3 - > $OUT/summary.txt <<'PY'
 import csv, re, collections
-O = "gpurun_out/r05c4p"
+O = "gpurun_out/c4_profile"
 log = open(f"{O}/ks.log").read()
 m = re.search(r"pairs (\d+)", log)
 pairs = int(m.group(1)) if m else None
 print("# config #4 (tools/c4_time.py: 3 solves), rocprofv3 kernel stats per solve")
-print(log.strip().splitlines()[-1] if log.strip() else "")
+print("\n".join(l for l in log.splitlines() if "config4 solve ms" in l))
 rows = sorted(csv.DictReader(open(f"{O}/ks/run_kernel_stats.csv")), key=lambda r: -float(r["TotalDurationNs"]))
 agg = collections.defaultdict(lambda: [0, 0.0])
 for r in rows:

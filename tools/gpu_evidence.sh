@@ -7,6 +7,8 @@
 #   5. PMC passes (one counter group each): FETCH_SIZE, WRITE_SIZE, the SQ
 #      issue/wait counters and the LDS bank-conflict counters of the hot kernels
 #   6. a HIP runtime trace of kp_place calls (hipMalloc / hipFree inside steps)
+#   7. config #4: per-kernel time and k_score_topk lane-ops per pair
+#      (gpu_c4_profile.sh) and the per-pass kernel trace (gpu_c4_trace.sh)
 set -o pipefail
 OUT=gpurun_out/evidence
 rm -rf $OUT; mkdir -p $OUT/prof $OUT/profsm $OUT/prof45 $OUT/pmc $OUT/rt
@@ -52,7 +54,20 @@ if [ -f $NOSEL ]; then
 fi
 timeout -k 10 300 rocprofv3 --hip-runtime-trace --kernel-trace --output-format csv -d $OUT/rt -o run -- python3 tools/place_steps.py > $OUT/rt/place.log 2>&1 || exit $?
 echo rt ok
-python3 tools/evidence_summary.py ${ROUND:-r04} $OUT $OUT/summary && ls $OUT/summary
+# config #4: per-kernel time per solve + k_score_topk lane-ops per pair, and
+# the per-pass / per-round kernel trace (SKIP_C4=1 skips)
+if [ "$SKIP_C4" != 1 ]; then
+  bash tools/gpu_c4_profile.sh > $OUT/c4_profile.log 2>&1 || { tail -5 $OUT/c4_profile.log; exit 1; }
+  SUFFIX=_ev bash tools/gpu_c4_trace.sh > $OUT/c4_trace.log 2>&1 || { tail -5 $OUT/c4_trace.log; exit 1; }
+  echo c4 ok
+fi
+python3 tools/evidence_summary.py ${ROUND:-r05} $OUT $OUT/summary && ls $OUT/summary
+R=${ROUND:-r05}
+if [ -f gpurun_out/c4_profile/summary.txt ]; then cp gpurun_out/c4_profile/summary.txt $OUT/summary/${R}_c4_profile.txt; fi
+if [ -f gpurun_out/c4t_ev/pass_sum.txt ]; then
+  { echo "# config #4 kernel trace of tools/c4_time.py (rocprofv3 --kernel-trace): per pass index, summed / largest k_accept and k_plan launch (tools/pass_trace_sum.py); then per-round kernel times (tools/round_kernel_sum.py)"
+    cat gpurun_out/c4t_ev/pass_sum.txt; echo; cat gpurun_out/c4t_ev/round_sum.txt; } > $OUT/summary/${R}_c4_pass_trace.txt
+fi
 # the raw traces exceed what gpurun copies back: keep logs and summaries only
 rm -f $OUT/prof/run_kernel_trace.csv $OUT/profsm/run_kernel_trace.csv $OUT/prof45/run_kernel_trace.csv $OUT/*/*/run_counter_collection.csv $OUT/*/*/run_kernel_trace.csv
 du -sh $OUT
