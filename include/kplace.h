@@ -238,7 +238,9 @@ int kp_score(kp_ctx *ctx, const kp_params *p, int32_t job_lo, int32_t job_hi,
  * round_up(N, 64): score_dev[(j-job_lo)*Ns + n] (padding columns
  * KP_SCORE_INFEASIBLE) and mask_dev[(j-job_lo)*(Ns/64) + n/64]. Either may be
  * NULL. Complete on return; with kp_set_profiling on, kp_last_timing reports
- * the kernels' HIP-event time (score_ms) and algorithmic bytes (score_bytes).
+ * the kernels' time (score_ms: the capacity-class kernel's own start / end
+ * stamps through hipExtLaunchKernel, HIP events around the launch for the
+ * other forms) and algorithmic bytes (score_bytes).
  * Not available on a kp_create_multi context (KP_EINVAL).
  */
 int kp_score_dev(kp_ctx *ctx, const kp_params *p, int32_t job_lo, int32_t job_hi,
