@@ -9,18 +9,22 @@
 //
 // k_score_topk: a 512-thread workgroup owns 1,024 columns (8 waves x 64 lanes
 // x 2 columns, tile operands in VGPRs) and streams its rows in chunks of 8:
-//   1. score — each wave computes the thresholds of its class for the
-//      chunk's rows (one exact division per (row, dim) lane), broadcasts them
-//      per row with v_readlane and writes its 128 scores of every row into a
-//      32-KB LDS tile;
+//   1. score — the chunk's row records (thresholds c - rho of the wave's
+//      capacity class, WQ, requests: k_unit_rec, once per solve; without
+//      them each wave computes its class's thresholds with one exact division
+//      per (row, dim) lane) reach LDS by DMA one chunk ahead; each wave
+//      writes its 128 scores of every row into the LDS tile (16-bit, double
+//      buffered when every score fits);
 //   2. select — wave w reads row w of the chunk back (16 columns per lane,
-//      strided over the tile; rows padded so that no LDS access conflicts):
-//      lane best of 32-bit truncated keys, bitonic sort of the 64 lane bests,
-//      T = the K-th of them (a lower bound of the tile's K-th key: K distinct
-//      columns reach it; truncation only keeps more), survivors >= T appended
-//      to LDS, exact ranks by counting; the tile's top-K exact keys, best
-//      first, go to part[row][tile]. More than 64 survivors (adversarial
-//      ties) switch to an exact bisection for the K-th 64-bit key.
+//      4-column groups strided over the tile; rows padded so that no LDS
+//      access conflicts): lane best of 32-bit truncated keys (and its best per
+//      group), T = the K-th lane best by a radix search over ballots (a lower
+//      bound of the tile's K-th key: K distinct columns reach it; truncation
+//      only keeps more), the survivors >= T of the groups whose best reached
+//      T appended to LDS, exact ranks from LDS broadcast reads; the tile's
+//      top-K exact keys, best first, go to part[row][tile]. More than 128
+//      survivors (adversarial ties) switch to an exact bisection for the K-th
+//      64-bit key.
 // k_merge_tour merges a row's per-tile lists into its K candidates, mapping
 // canonical position -> node through perm. Bit-exact with the materialised
 // path (k_score32 + k_select_t) and oracle kpo_round_candidates: every
