@@ -20,6 +20,8 @@ Beside the step (same run, outside the timed steps):
   score_matrix    the materialised int32 score matrix + feasibility bitmask
                   of the whole queue (kp_score_dev; on N GPUs each rank its
                   row block) against the HBM roofline;
+  config2         BASELINE config #2 (10k x 1k bin-pack, 1 GPU): device solve,
+                  pairs/s, host->host latency, the oracle on the same snapshot;
   config4         BASELINE config #4 (200k x 20k, running jobs filling every
                   dim to >= 30% of its capacity): solve + kp_preempt on the
                   same N GPUs (row-sharded, collective), with its phase split
@@ -207,13 +209,20 @@ def streaming_cpu(args, cap, topo, req, prio, p):
                       f"trace (batch 0 only on 1 thread); GPU leg: all batches", **out}
 
 
-def config4_cpu(args, w, p):
-    """The oracle beside the config #4 leg (bounded sample; the full 200k x 20k
-    solve + preemption takes the oracle ~25 min on 6 cores): the first
-    `--cpu-c4-jobs` pending jobs of the same snapshot (same nodes, same
-    running jobs and usage), the first `--cpu-c4-rounds` rounds of their
-    solve, then the preemption nominations (kpo_preempt), on every host core
-    and on 1 thread. Reported as scored job-node pairs per second."""
+def config4_cpu(args, w, p, post=None):
+    """The oracle beside the config #4 leg (bounded samples; the full 200k x 20k
+    solve + preemption takes the oracle ~25 min on 6 cores), on every host
+    core and on 1 thread, as scored job-node pairs per second:
+      solve    the first `--cpu-c4-jobs` pending jobs of the same snapshot
+               (same nodes, running jobs and usage), the first
+               `--cpu-c4-rounds` rounds of their solve;
+      preempt  (`post`: the GPU leg's final solve, node usage and status)
+               the first `--cpu-c4-preemptors` of the GPU leg's actual
+               preemptors (NO_FIT singletons) against the full node pool at
+               the GPU solve's post-solve usage, with the same running jobs:
+               kpo_preempt (its solve of these rows is one round in which
+               every row is NO_FIT) minus kpo_place of the same snapshot =
+               the preemption scoring alone."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_bind as ob
     Js = min(args.cpu_c4_jobs, w.J)
@@ -225,17 +234,91 @@ def config4_cpu(args, w, p):
     for label, threads in (("all_cores", host_cores()), ("single", 1)):
         progress(f"cpu baseline (config #4): oracle on {threads} thread(s), {Js} jobs")
         t = time.perf_counter()
-        r, pr = ob.preempt(sb, p, m["run_node"], m["run_req"], m["run_prio"], nthreads=threads)
+        r = ob.place(sb, p, nthreads=threads)
         dt = time.perf_counter() - t
         out[label] = {"threads": threads, "seconds": dt, "rounds": r["rounds"],
-                      "placed_jobs": r["placed"], "preemptors": pr["preemptors"],
-                      "pairs_per_s": (float(r["pairs"]) + float(pr["pairs"])) / dt}
+                      "placed_jobs": r["placed"], "pairs_per_s": float(r["pairs"]) / dt}
+    pre = None
+    if post is not None:
+        pj = np.flatnonzero((post["status"] == _abi.KP_JOB_NO_FIT) & (w.gang_size == 1))
+        pj = pj[:args.cpu_c4_preemptors]
+        sp = ob.SnapshotBuf(np.ascontiguousarray(w.req[:, pj]), w.cap, post["used"], w.prio[pj],
+                            topo=w.topo)
+        p1 = _abi.default_params(**synth.CONFIG_PARAMS[4])
+        pre = {"sample": f"the first {pj.size} of the GPU leg's {post['preemptors']} preemptors "
+                         f"(NO_FIT singletons, job order) against all {w.N} nodes at the GPU "
+                         f"solve's post-solve usage, {m['run_node'].size} running jobs"}
+        for label, threads in (("all_cores", host_cores()), ("single", 1)):
+            progress(f"cpu baseline (config #4 preemption): oracle on {threads} thread(s), "
+                     f"{pj.size} preemptors")
+            t = time.perf_counter()
+            r = ob.place(sp, p1, nthreads=threads)
+            t_place = time.perf_counter() - t
+            t = time.perf_counter()
+            r2, pr = ob.preempt(sp, p1, m["run_node"], m["run_req"], m["run_prio"], nthreads=threads)
+            t_all = time.perf_counter() - t
+            dt = max(t_all - t_place, 1e-9)
+            pre[label] = {"threads": threads, "seconds": dt, "preemptors": pr["preemptors"],
+                          "nominated": pr["nominated"], "placed_in_sample": r2["placed"],
+                          "pairs_per_s": float(pr["pairs"]) / dt}
+        pre["value"] = pre["all_cores"]["pairs_per_s"]
     return {"value": out["all_cores"]["pairs_per_s"], "unit": "pairs/s", "cores": host_cores(),
             "kind": "port", "cpu_model": cpu_model(),
             "sample": f"oracle/kp_oracle.c: the first {args.cpu_c4_rounds} rounds of the solve of "
                       f"the first {Js} of the {w.J} pending jobs against the same {w.N}-node "
-                      f"snapshot and running jobs, then kpo_preempt; pairs = scored job-node "
-                      f"pairs of the solve + preemption", **out}
+                      f"snapshot and running jobs; pairs = scored job-node pairs of the solve; "
+                      f"preemption: see preempt.sample", **out, "preempt": pre}
+
+
+def config2(args, make_placer):
+    """BASELINE config #2 (10k jobs x 1k nodes x 4 dims, bin-pack score only,
+    singletons, empty cluster, 1 GPU): device solve on the resident snapshot
+    (kp_reset_nodes + kp_solve, the headline's step), host->host kp_place
+    latency, and the oracle beside it on the SAME full snapshot (1 thread and
+    every host core; small enough to run whole)."""
+    w = synth.config2(args.c2_jobs, args.c2_nodes)
+    p = _abi.default_params(**synth.CONFIG_PARAMS[2])
+    with make_placer() as pl:
+        pl.load_nodes(w.cap, w.used, w.topo)
+        pl.load_jobs(w.req, w.prio, w.gang_id, w.gang_size)
+        for _ in range(3):  # warmup
+            pl.reset_nodes()
+            pl.solve(p)
+        t = time.perf_counter()
+        for _ in range(args.c2_steps):
+            pl.reset_nodes()
+            st = pl.solve(p)
+        s_ms = 1e3 * (time.perf_counter() - t) / args.c2_steps
+        lat = []
+        for _ in range(args.c2_steps):
+            t = time.perf_counter()
+            g = pl.place(w, p)
+            lat.append(time.perf_counter() - t)
+    cpu = None
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_bind as ob
+        sb = ob.SnapshotBuf.from_workload(w)
+        cpu = {"unit": "pairs/s", "kind": "port", "cpu_model": cpu_model(), "cores": host_cores(),
+               "sample": f"oracle/kp_oracle.c full placement of the same config2 {w.J}x{w.N} "
+                         f"snapshot (the whole workload, not a sample)"}
+        for label, threads in (("all_cores", host_cores()), ("single", 1)):
+            progress(f"cpu baseline (config #2): oracle on {threads} thread(s)")
+            t = time.perf_counter()
+            o = ob.place(sb, p, nthreads=threads)
+            dt = time.perf_counter() - t
+            cpu[label] = {"threads": threads, "ms": 1e3 * dt, "pairs_per_s": float(w.J) * w.N / dt,
+                          "rounds": o["rounds"], "placed_jobs": o["placed"]}
+        cpu["value"] = cpu["all_cores"]["pairs_per_s"]
+        cpu["same_placement"] = bool(np.array_equal(o["node"], g["node"]))
+    return {"config": f"#2 bin-pack: {w.J} jobs x {w.N} nodes x 4 dims, singletons, empty cluster, "
+                      f"w_dim (1,1,1,1), no GPU-fit / spread",
+            "solve_ms": s_ms, "pairs_per_s": float(w.J) * w.N / (s_ms / 1e3),
+            "pairs_scored_per_s": float(st["pairs"]) / (s_ms / 1e3),
+            "latency_ms": 1e3 * float(np.median(lat)),
+            "latency_def": f"kp_place host->host, median of {len(lat)}",
+            "rounds": st["rounds"], "passes": st["passes"], "placed_jobs": st["placed"],
+            "steps": args.c2_steps, "cpu_baseline": cpu}
 
 
 def phase_split(pl, p, sync=lambda x: x, gather=lambda d: [d]) -> dict:
@@ -248,15 +331,17 @@ def phase_split(pl, p, sync=lambda x: x, gather=lambda d: [d]) -> dict:
     pl.reset_nodes()
     pl.set_profiling(2)
     st = pl.solve(p)
-    tm = pl.timing()
+    shards = pl.timing_shards()  # one per kp_create_multi shard, else this rank's
     pl.set_profiling(False)
-    mine = {"solve_ms": tm["solve_ms"], "cand_ms": tm["cand_ms"], "xchg_ms": tm["xchg_ms"],
-            "pass_ms": tm["pass_ms"], "rounds": st["rounds"]}
-    ranks = gather(mine)
+    mine = [{"solve_ms": tm["solve_ms"], "cand_ms": tm["cand_ms"], "xchg_ms": tm["xchg_ms"],
+             "pass_ms": tm["pass_ms"], "rccl_calls": tm["rccl_calls"], "rounds": st["rounds"]}
+            for tm in shards]
+    ranks = [r for rk in gather(mine) for r in rk]
     out = {k: max(r[k] for r in ranks) for k in ("solve_ms", "cand_ms", "xchg_ms", "pass_ms")}
-    out.update(rounds=st["rounds"], per_rank=ranks,
+    out.update(rounds=st["rounds"], per_rank=ranks, rccl_calls=ranks[0]["rccl_calls"],
                note="device time from HIP events at each round's phase boundaries (their own "
-                    "records add a few us per round); max over ranks")
+                    "records add a few us per round); max over ranks (or kp_create_multi shards); "
+                    "rccl_calls = ncclAllGather calls of the solve (one per round over RCCL)")
     return out
 
 
@@ -276,6 +361,7 @@ def config4(args, make_placer, n_gpus=1, barrier=lambda: None, max_over_ranks=la
         pl.load_running(m["run_node"], m["run_req"], m["run_prio"])
         pl.load_jobs(w.req, w.prio, w.gang_id, w.gang_size)
         sol, pre = [], []
+        post = None
         for it in range(args.c4_steps + 1):
             progress(f"config #4 step {it}")
             pl.reset_nodes()
@@ -290,6 +376,9 @@ def config4(args, make_placer, n_gpus=1, barrier=lambda: None, max_over_ranks=la
             if it:  # first iteration: warmup
                 sol.append(max_over_ranks(t1 - t0))
                 pre.append(max_over_ranks(t2 - t1b))
+        if n_gpus == 1 and not args.no_cpu_baseline:  # the CPU preemption sample's rows + usage
+            g = pl.fetch()
+            post = {"status": g["status"], "used": g["used"], "preemptors": pr["preemptors"]}
         phases = None
         if not args.no_phases:
             progress("config #4 phase split")
@@ -298,7 +387,7 @@ def config4(args, make_placer, n_gpus=1, barrier=lambda: None, max_over_ranks=la
             phases["preempt_ms"] = 1e3 * float(np.mean(pre))
     s_ms, p_ms = 1e3 * float(np.mean(sol)), 1e3 * float(np.mean(pre))
     util = w.used.sum(1) / w.cap.sum(1)
-    cpu = None if args.no_cpu_baseline or n_gpus > 1 else config4_cpu(args, w, p)
+    cpu = None if args.no_cpu_baseline or n_gpus > 1 else config4_cpu(args, w, p, post)
     return {"config": f"#4 preemption: {w.J} pending x {w.N} nodes, {m['run_node'].size} running "
                       f"jobs; occupancy per dim (cpu, mem, gpu, gpu_mem) "
                       f"{', '.join(f'{x:.3f}' for x in util)} (every dim >= 0.30)",
@@ -309,7 +398,8 @@ def config4(args, make_placer, n_gpus=1, barrier=lambda: None, max_over_ranks=la
             "cpu_baseline": cpu,
             "rounds": st["rounds"], "passes": st["passes"], "placed_jobs": st["placed"],
             "preemptors": pr["preemptors"], "nominated": pr["nominated"],
-            "preempt_pairs": pr["pairs"], "steps": args.c4_steps, "phases": phases}
+            "preempt_pairs": pr["pairs"], "preempt_pairs_per_s": float(pr["pairs"]) / (p_ms / 1e3),
+            "steps": args.c4_steps, "phases": phases}
 
 
 def score_matrix(args, make_placer, w, p, rank=0, world=1, gather=lambda d: [d]):
@@ -418,6 +508,12 @@ def main():
                     help="config #4 CPU baseline sample: the first N pending jobs")
     ap.add_argument("--cpu-c4-rounds", type=int, default=3,
                     help="config #4 CPU baseline sample: rounds of their solve")
+    ap.add_argument("--cpu-c4-preemptors", type=int, default=2_000,
+                    help="config #4 CPU preemption sample: the first N of the GPU leg's preemptors")
+    ap.add_argument("--c2-jobs", type=int, default=10_000)
+    ap.add_argument("--c2-nodes", type=int, default=1_000)
+    ap.add_argument("--c2-steps", type=int, default=20)
+    ap.add_argument("--no-config2", action="store_true")
     ap.add_argument("--cpu-stream-batches", type=int, default=4,
                     help="config #5 CPU baseline sample: the first N micro-batches")
     ap.add_argument("--no-phases", action="store_true",
@@ -556,6 +652,9 @@ def main():
         progress("score matrix leg")
         legs["score_matrix"] = score_matrix(args, make_local if n_gpus > 1 else make_placer, w, p,
                                             rank=rank, world=world, gather=gather)
+    if not args.no_config2 and n_gpus == 1:
+        progress("config #2 leg")
+        legs["config2"] = config2(args, make_placer)
     if not args.no_config4:
         progress("config #4 leg")
         legs["config4"] = config4(args, make_placer, n_gpus, barrier, max_over_ranks, gather)

@@ -33,13 +33,16 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 7  /* 4: kp_last_error_r; 5: kp_timing.incr_rounds;
+#define KP_ABI_VERSION 8  /* 4: kp_last_error_r; 5: kp_timing.incr_rounds;
                               6: kp_score_dev, kp_timing.score_form / score_classes;
                               7: kp_timing phase split (cand/xchg/pass_ms,
                                  kp_set_profiling level 2); kp_load_running and
                                  kp_preempt are collective on world_size > 1
                                  contexts (every rank calls them, in the same
-                                 order as its kp_solve calls) */
+                                 order as its kp_solve calls);
+                              8: kp_timing.rccl_calls (was padding),
+                                 kp_last_timing_shards; kp_last_timing on a
+                                 kp_create_multi context = max over shards */
 
 /* ---- limits ------------------------------------------------------------ */
 #define KP_MAX_DIMS 8       /* resource dimensions per job/node               */
@@ -307,7 +310,10 @@ typedef struct kp_timing {
                                0 = the per-wave uniform / mixed form */
   int32_t score_classes;    /* capacity classes of the node table (0: more than
                                the class form handles) */
-  int32_t pad;
+  int32_t rccl_calls;       /* ncclAllGather calls since the last kp_solve
+                               started (its rounds' exchanges + any kp_preempt
+                               after it); 0 without an RCCL communicator.
+                               Counted at every profiling level.             */
   /* level 2 only (else 0), summed over the solve's rounds: */
   double cand_ms;           /* candidate phase: round start (active-unit
                                compaction, node pack) + filter/score/top-K +
@@ -316,7 +322,14 @@ typedef struct kp_timing {
                                + all-gather + unpack (0 on one GPU)          */
   double pass_ms;           /* bidder index + plan/accept passes + commit    */
 } kp_timing;
+/* On a kp_create_multi context: every time field is the slowest shard's (the
+   max per field), score_launches / score_bytes / select_bytes the sum over
+   shards, the other fields shard 0's. */
 int kp_last_timing(kp_ctx *ctx, kp_timing *t);
+/* Per-shard timing: fills t[0 .. min(n, shards) - 1] in shard order and
+   returns the number of shards (1 for a one-GPU / one-rank context; n = 0
+   only asks for the count). Negative KP_E* on failure. */
+int kp_last_timing_shards(kp_ctx *ctx, kp_timing *t, int32_t n);
 
 /* HIP-event timing: 0 off (default), 1 the filter+score launches, 2 also the
    per-round phase split (kp_timing.cand/xchg/pass_ms). Both add event records

@@ -62,7 +62,7 @@ struct Entry {
 
 // KP_DEBUG_KNOBS=1 is the only environment variable the product reads; the
 // tuning / A/B / test knobs below it are ignored without it
-static const char *knob(const char *name) {
+const char *knob(const char *name) {
   const char *on = std::getenv("KP_DEBUG_KNOBS");
   return on && std::strcmp(on, "1") == 0 ? std::getenv(name) : nullptr;
 }
@@ -198,7 +198,7 @@ static int ensure_units(kp_ctx *c, int32_t U, int32_t J) {
     KP_TRY(dalloc(&c->d.stats, 1));
     c->d.temp_bytes = rocprim_temp_bytes((int32_t)std::min<size_t>(pm, INT32_MAX));
     KP_TRY(dalloc(reinterpret_cast<uint8_t **>(&c->d.temp), c->d.temp_bytes));
-    if (c->world > 1) {
+    if (c->xchg) {
       KP_TRY(dalloc(&c->d.act, u));
       KP_TRY(dalloc(&c->d.cand, u * K));
       KP_TRY(dalloc(&c->d.xg_counts, (size_t)c->world));
@@ -375,9 +375,15 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   }
   c->hpass = c->pinned_coh + 32;
   for (int i = 0; i < 64; ++i) c->hpass[i] = -1;  // never a tag (tags are even, >= 0)
+  // KP_RCCL_SOLO=1 (tests): a one-rank context given an RCCL id builds a
+  // one-rank communicator and runs the multi-rank solve (pack -> ncclAllGather
+  // -> unpack every round, the preemption all-gather), so that the RCCL path
+  // executes on a one-GPU box exactly as each rank of an N-GPU job runs it
+  const char *solo_env = knob("KP_RCCL_SOLO");
+  const bool solo = solo_env && std::atoi(solo_env) != 0;
   if (nccl_comm) {
     c->nccl_comm = nccl_comm;
-  } else if (world > 1 && nccl_id) {  // else: host-staged exchange (kp_set_allgather)
+  } else if ((world > 1 || solo) && nccl_id) {  // else: host-staged exchange (kp_set_allgather)
     ncclUniqueId id;
     std::memcpy(&id, nccl_id, sizeof id);
     ncclComm_t comm;
@@ -387,6 +393,7 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
     }
     c->nccl_comm = comm;
   }
+  c->xchg = world > 1 || c->nccl_comm != nullptr;
   *out = c;
   return KP_OK;
 }
@@ -539,8 +546,18 @@ static int load_nodes_impl(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap,
                           hipMemcpyHostToDevice, c->stream));
     KP_HIP(hipMemcpyAsync(c->d.wshift, wshift.data(), sizeof(int32_t) * (fz_P / 128),
                           hipMemcpyHostToDevice, c->stream));
-    KP_TRY(dalloc(&c->d.tcls, (size_t)fz_P / 128));
-    KP_TRY(dalloc(&c->d.fccap, std::max<size_t>(fccap.size(), 1)));
+    // grow-only, like colnode: a reload of the same table shape allocates
+    // nothing (hipFree synchronises the device)
+    if ((int64_t)fz_P / 128 > c->cap_tcls) {
+      c->cap_tcls = 0;
+      KP_TRY(dalloc(&c->d.tcls, (size_t)fz_P / 128));
+      c->cap_tcls = fz_P / 128;
+    }
+    if ((int64_t)std::max<size_t>(fccap.size(), 1) > c->cap_fccap) {
+      c->cap_fccap = 0;
+      KP_TRY(dalloc(&c->d.fccap, std::max<size_t>(fccap.size(), 1)));
+      c->cap_fccap = (int64_t)std::max<size_t>(fccap.size(), 1);
+    }
     KP_HIP(hipMemcpyAsync(c->d.tcls, tcls.data(), sizeof(int32_t) * (fz_P / 128),
                           hipMemcpyHostToDevice, c->stream));
     KP_HIP(hipMemcpyAsync(c->d.fccap, fccap.data(), sizeof(uint32_t) * fccap.size(),
@@ -775,6 +792,7 @@ static int allgather_i32(kp_ctx *c, const int32_t *send, int32_t *recv, size_t p
     if (c->peer_failed && c->peer_failed->load(std::memory_order_acquire))
       return fail(KP_ERCCL, "a peer shard failed before the exchange");
     c->in_collective = true;
+    c->rccl_calls++;
     if (ncclAllGather(send, recv, per, ncclInt32, static_cast<ncclComm_t>(c->nccl_comm),
                       c->stream) != ncclSuccess)
       return fail(KP_ERCCL, "ncclAllGather of %zu ints", per);
@@ -816,13 +834,14 @@ static double ev_ms(hipEvent_t a, hipEvent_t b) {
 
 static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   if (!c->nodes_loaded || !c->jobs_loaded) return fail(KP_ESTATE, "kp_solve: load nodes and jobs first");
-  if (c->world > 1 && !c->nccl_comm && !c->allgather)
+  if (c->xchg && !c->nccl_comm && !c->allgather)
     return fail(KP_ESTATE, "kp_solve: multi-rank context without an exchange");
   KP_TRY(check_params(p, c->D));
   c->solved = false;
   // per-solve state that an earlier failed solve may have left set
   c->keys_in_merge = false;
   c->in_collective = false;
+  c->rccl_calls = 0;
   KP_HIP(hipSetDevice(c->device));
   const ScoreParams sp = make_sp(c, p);
   const int32_t K = p->n_cand, U = c->U, N = c->N;
@@ -873,11 +892,19 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     if (c->nfc > 0 && c->crec_enabled && words * 4 <= c->crec_max_bytes) {
       if (words > c->cap_crec) {
         c->cap_crec = 0;
-        KP_TRY(dalloc(&c->d.crec, (size_t)words));
-        c->cap_crec = words;
+        if (dalloc(&c->d.crec, (size_t)words) == KP_OK) {
+          c->cap_crec = words;
+        } else {
+          // the table is an optimisation: k_score_topk computes the records
+          // itself without it, so a short device does not fail the solve
+          (void)hipGetLastError();
+          c->last_error.clear();
+        }
       }
-      KP_TRY(launch_unit_rec(c, sp));
-      c->crec_ok = true;
+      if (c->cap_crec >= words) {
+        KP_TRY(launch_unit_rec(c, sp));
+        c->crec_ok = true;
+      }
     }
     rpc = INT64_MAX;  // no matrix, no chunks: per row only tiles x K keys
     KP_TRY(ensure_part(c, (int64_t)std::max(shard, 1) * (c->fz_P / fz_tile(c)) * K));
@@ -933,7 +960,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     if (fused) {
       // one GPU, counting mode: the merge also does k_csr_keys' work
       c->keys_in_merge = false;
-      if (c->world == 1 && c->keys_merge_enabled && r0 == 0 && rows > 0) {
+      if (!c->xchg && c->keys_merge_enabled && r0 == 0 && rows > 0) {
         KP_TRY(csr_prepare(c, rows, K));
         c->keys_in_merge = c->csr_mode == 1;
       }
@@ -1026,7 +1053,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
     }
     return KP_OK;
   };
-  if (c->world == 1) {
+  if (!c->xchg) {
     // Device-driven rounds: a round is enqueued with its grids sized by the
     // previous round's active count (active units only shrink) and every
     // kernel clamps to the device count. The host learns a round's count
@@ -1164,7 +1191,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
   }
   KP_TRY(launch_finalize(c));
   KP_HIP(hipEventRecord(t1, c->stream));
-  if (c->host_prof && c->world == 1) {
+  if (c->host_prof && !c->xchg) {
     launch_probe(c, sp, std::min<int32_t>(shard, 26000));
     launch_probe(c, sp, std::min<int32_t>(shard, 1000));
   }
@@ -1175,7 +1202,7 @@ static int solve_impl(kp_ctx *c, const kp_params *p, kp_result *stats) {
                           c->stream));
   SolveStats dst{};
   KP_HIP(hipMemcpyAsync(&dst, c->d.stats, sizeof dst, hipMemcpyDeviceToHost, c->stream));
-  if (c->world > 1) {
+  if (c->xchg) {
     hipEvent_t evF;
     KP_TRY(E.make(&evF, hipEventDisableTiming));
     KP_TRY(wait_stream(c, evF));
@@ -1409,10 +1436,8 @@ void kp_destroy(kp_ctx *c) {
                   d.bm, d.bms, d.rowinfo, d.cnt, d.rowmap, d.tcls, d.fccap, d.crec};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
-  if (c->world > 1) {
-    if (d.act) (void)hipFree(d.act);
-    if (d.cand) (void)hipFree(d.cand);
-  }
+  if (d.act && d.act != d.act_local) (void)hipFree(d.act);  // multi-rank: separate buffers
+  if (d.cand && d.cand != d.cand_local) (void)hipFree(d.cand);
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->pinned_coh) (void)hipHostFree(c->pinned_coh);
   if (c->stage) (void)hipHostFree(c->stage);
@@ -1438,12 +1463,53 @@ int kp_set_profiling(kp_ctx *c, int level) {
   return KP_OK;
 }
 
+// every shard's kp_timing of a kp_create_multi context (shard order)
+static int shard_timings(kp_ctx *c, std::vector<kp_timing> &all) {
+  all.assign((size_t)c->world, kp_timing{});
+  return multi_run(c, [&](kp_ctx *sh, int i) { return kp_last_timing(sh, &all[(size_t)i]); }, true);
+}
+
 int kp_last_timing(kp_ctx *c, kp_timing *t) {
   if (!c || !t) return KP_EINVAL;
-  if (c->multi) return multi_run(c, [&](kp_ctx *sh, int) { return kp_last_timing(sh, t); }, false);
+  if (c->multi) {
+    // the shards run concurrently: times are the slowest shard's (max per
+    // field, like the one-process-per-GPU bench's max over ranks), counts and
+    // bytes the sum over shards, the form fields shard 0's
+    std::vector<kp_timing> all;
+    KP_TRY(shard_timings(c, all));
+    kp_timing m = all[0];
+    for (size_t i = 1; i < all.size(); ++i) {
+      const kp_timing &s = all[i];
+      m.solve_ms = std::max(m.solve_ms, s.solve_ms);
+      m.score_ms = std::max(m.score_ms, s.score_ms);
+      m.select_ms = std::max(m.select_ms, s.select_ms);
+      m.accept_ms = std::max(m.accept_ms, s.accept_ms);
+      m.cand_ms = std::max(m.cand_ms, s.cand_ms);
+      m.xchg_ms = std::max(m.xchg_ms, s.xchg_ms);
+      m.pass_ms = std::max(m.pass_ms, s.pass_ms);
+      m.score_launches += s.score_launches;
+      m.score_bytes += s.score_bytes;
+      m.select_bytes += s.select_bytes;
+    }
+    *t = m;
+    return KP_OK;
+  }
   Entry en(c);
   *t = c->timing;
+  t->rccl_calls = c->rccl_calls;  // the solve's, plus any kp_preempt since
   return KP_OK;
+}
+
+int kp_last_timing_shards(kp_ctx *c, kp_timing *t, int32_t n) {
+  if (!c || n < 0 || (n > 0 && !t)) return KP_EINVAL;
+  if (!c->multi) {
+    if (n > 0) KP_TRY(kp_last_timing(c, t));
+    return 1;
+  }
+  std::vector<kp_timing> all;
+  KP_TRY(shard_timings(c, all));
+  for (int32_t i = 0; i < n && i < (int32_t)all.size(); ++i) t[i] = all[(size_t)i];
+  return (int)all.size();
 }
 
 // ---------------------------------------------------------------------------
@@ -1631,7 +1697,8 @@ int kp_score_dev(kp_ctx *c, const kp_params *p, int32_t job_lo, int32_t job_hi,
   tm.score_classes = c->n_classes;
   tm.score_form = c->fits32 && c->n_classes > 0 && c->score_classes ? 1 : 0;
   c->timing = tm;
-  if (rows == 0 || N == 0) return KP_OK;
+  // nothing to write: no launch (and no profiling events left unrecorded)
+  if (rows == 0 || N == 0 || (!score_dev && !mask_dev)) return KP_OK;
   KP_TRY(prep_for(c, p));
   const ScoreParams sp = make_sp(c, p);
   const int64_t Ns = (N + 63) & ~63, words = Ns / 64;
@@ -1653,7 +1720,10 @@ int kp_score_dev(kp_ctx *c, const kp_params *p, int32_t job_lo, int32_t job_hi,
   // on the device): the grid's last partial wave of workgroups is paid once,
   // not once per cap_U-row chunk (tools/score_roof.hip: 4 chunks cost 0.74 ->
   // 0.78 ms of stores alone and more with the score arithmetic). Chunks only
-  // past the grid's y limit (65,535 row blocks of 64 rows).
+  // past the grid's y limit of 65,535 row blocks: the 32-bit forms take 64
+  // (k_score32c) or 128 (k_score32) rows per block at that size, the 64-bit
+  // k_score always 32.
+  const int64_t chunk = (int64_t)65535 * (c->fits32 ? 64 : 32);
   if (c->cap_rowmap < rows) {
     c->cap_rowmap = 0;
     KP_TRY(dalloc(&c->d.rowmap, (size_t)rows));
@@ -1662,7 +1732,6 @@ int kp_score_dev(kp_ctx *c, const kp_params *p, int32_t job_lo, int32_t job_hi,
   KP_HIP(hipMemcpyAsync(c->d.rowmap, unit_of.data(), sizeof(int32_t) * rows, hipMemcpyHostToDevice,
                         c->stream));
   Events E;
-  const int64_t chunk = (int64_t)65535 * 64;
   for (int64_t r0 = 0; r0 < rows; r0 += chunk) {
     const int32_t nr = (int32_t)std::min<int64_t>(chunk, rows - r0);
     // profiling: the kernel's own start / end stamps (hipExtLaunchKernel),
@@ -1815,7 +1884,7 @@ int kp_preempt(kp_ctx *c, kp_preemption *out) {
   KP_HIP(hipSetDevice(c->device));
   int32_t P = 0, lo = 0, hi = 0;
   KP_TRY(launch_preempt(c, &P, &lo, &hi));
-  if (c->world > 1 && P > 0) {
+  if (c->xchg && P > 0) {
     // rank r scored rows [lo, hi): one all-gather of B = ceil(P / world) rows
     // per rank gives every rank every nomination
     if (!c->nccl_comm && !c->allgather)
@@ -1848,7 +1917,7 @@ int kp_preempt(kp_ctx *c, kp_preemption *out) {
   if (J > 0)
     KP_HIP(hipMemcpyAsync(nom.data(), c->d.pre_node, sizeof(int32_t) * J, hipMemcpyDeviceToHost,
                           c->stream));
-  if (c->world > 1) {
+  if (c->xchg) {
     hipEvent_t ev;
     Events E;
     KP_TRY(E.make(&ev, hipEventDisableTiming));

@@ -194,6 +194,11 @@ struct kp_ctx {
   int device = 0;
   int world = 1, rank = 0;
   void *nccl_comm = nullptr;  // ncclComm_t
+  // the solve runs the multi-rank form (act/cand exchanged once per round,
+  // preemption rows all-gathered): world > 1, or a one-rank RCCL communicator
+  // (KP_RCCL_SOLO=1, tests: the RCCL exchange executed on a one-GPU box)
+  bool xchg = false;
+  int32_t rccl_calls = 0;  // ncclAllGather calls of the current / last solve
   // host-staged exchange (kp_set_allgather) when world > 1 without RCCL
   kp_allgather_fn allgather = nullptr;
   void *allgather_user = nullptr;
@@ -259,6 +264,7 @@ struct kp_ctx {
   int64_t cap_P = 0;           // columns of d.np32
   int64_t cap_part = 0;        // entries of d.part
   int64_t cap_fz = 0;          // columns of d.colnode
+  int64_t cap_tcls = 0, cap_fccap = 0;  // entries of d.tcls / d.fccap
   // fused score + top-K (k_score_topk): columns of the class-aligned layout,
   // whether that layout is compact enough to use, KP_FUSED=0 disables it
   int32_t fz_P = 0;
@@ -389,6 +395,8 @@ int launch_preempt_pack(kp_ctx *c, int32_t lo, int32_t hi, int32_t *send);
 int launch_preempt_unpack(kp_ctx *c, int32_t P, int32_t B, const int32_t *recv);
 int launch_delta(kp_ctx *c, int32_t K, int32_t *bad_host);
 
+// the value of a tuning / test knob: read only under KP_DEBUG_KNOBS=1, else NULL
+const char *knob(const char *name);
 // context over one GPU (kp_api.cpp); nccl_comm, if given, is adopted
 int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_id,
                void *nccl_comm, int64_t max_pairs);

@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <thread>
@@ -217,7 +218,11 @@ int multi_create(kp_ctx **out, const int32_t *ids, int32_t n, int64_t max_pairs)
   c->device = devs[0];
   c->world = n;
   std::vector<ncclComm_t> comms(n, nullptr);
-  if (n > 1 && distinct) {
+  // KP_RCCL_SOLO=1 (tests): kp_create_multi([g]) builds its one communicator
+  // through ncclCommInitAll too and runs the RCCL exchange on one GPU
+  const char *solo_env = knob("KP_RCCL_SOLO");
+  const bool solo = n == 1 && solo_env && std::atoi(solo_env) != 0;
+  if ((n > 1 || solo) && distinct) {
     if (ncclCommInitAll(comms.data(), n, devs.data()) != ncclSuccess) {
       multi_destroy(c);
       return KP_ERCCL;

@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-KP_ABI_VERSION = 7
+KP_ABI_VERSION = 8
 KP_MAX_DIMS = 8
 KP_MAX_CAND = 32
 KP_MAX_GANG = 64
@@ -95,7 +95,7 @@ class Timing(C.Structure):
         ("select_ms", C.c_double), ("accept_ms", C.c_double),
         ("score_launches", C.c_int64), ("score_bytes", C.c_int64),
         ("select_bytes", C.c_int64), ("fused", C.c_int32), ("score_form", C.c_int32),
-        ("score_classes", C.c_int32), ("pad", C.c_int32),
+        ("score_classes", C.c_int32), ("rccl_calls", C.c_int32),
         ("cand_ms", C.c_double), ("xchg_ms", C.c_double), ("pass_ms", C.c_double),
     ]
 
@@ -178,6 +178,7 @@ def load_library(path: str | None = None) -> C.CDLL:
         "kp_score": (C.c_int, [vp, C.POINTER(Params), C.c_int32, C.c_int32, _i32p, _u64p]),
         "kp_score_dev": (C.c_int, [vp, C.POINTER(Params), C.c_int32, C.c_int32, vp, vp]),
         "kp_last_timing": (C.c_int, [vp, C.POINTER(Timing)]),
+        "kp_last_timing_shards": (C.c_int, [vp, C.POINTER(Timing), C.c_int32]),
         "kp_set_profiling": (C.c_int, [vp, C.c_int]),
         "kp_set_allgather": (C.c_int, [vp, ALLGATHER_FN, vp]),
         "kp_parse_gpu_memory": (C.c_int, [C.c_char_p, _i64p]),
@@ -199,6 +200,6 @@ EXPORTED = (
     "kp_last_error", "kp_last_error_r",
     "kp_abi_version", "kp_dist_unique_id", "kp_place", "kp_load_nodes",
     "kp_load_jobs", "kp_solve", "kp_fetch", "kp_apply_delta", "kp_reset_nodes", "kp_score",
-    "kp_last_timing", "kp_set_profiling", "kp_parse_gpu_memory", "kp_load_running",
+    "kp_last_timing", "kp_last_timing_shards", "kp_set_profiling", "kp_parse_gpu_memory", "kp_load_running",
     "kp_preempt", "kp_set_allgather", "kp_score_dev",
 )

@@ -225,6 +225,16 @@ class Placer:
         _check(lib().kp_last_timing(self._h, C.byref(t)), "kp_last_timing", self._h)
         return {k: getattr(t, k) for k, _ in _abi.Timing._fields_}
 
+    def timing_shards(self) -> list:
+        """kp_last_timing_shards: one timing dict per shard (kp_create_multi),
+        a single one for a one-GPU / one-rank context."""
+        n = lib().kp_last_timing_shards(self._h, None, 0)
+        _check(min(n, 0), "kp_last_timing_shards", self._h)
+        ts = (_abi.Timing * n)()
+        got = lib().kp_last_timing_shards(self._h, ts, n)
+        _check(min(got, 0), "kp_last_timing_shards", self._h)
+        return [{k: getattr(t, k) for k, _ in _abi.Timing._fields_} for t in ts]
+
     # ---- one-shot ----------------------------------------------------------
     def place(self, w, params: _abi.Params) -> dict:
         """kp_place on a synth.Workload-like object (req/cap/used/prio/gang_id/

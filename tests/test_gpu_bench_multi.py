@@ -68,8 +68,9 @@ def test_bench_multi_rank_rehearsal(want, extra, config4):
     assert (c["rounds"], c["passes"], c["placed_jobs"]) == (want["rounds"], want["passes"], want["placed"])
     assert b["latency_ms"] > 0
     ph = b["phases"]
-    # one process per rank reports every rank; --single-process one (shard 0)
-    assert ph["rounds"] == want["rounds"] and len(ph["per_rank"]) == (1 if "--single-process" in extra else 2)
+    # one process per rank reports every rank, --single-process every shard
+    # (kp_last_timing_shards)
+    assert ph["rounds"] == want["rounds"] and len(ph["per_rank"]) == 2
     assert ph["cand_ms"] > 0 and ph["xchg_ms"] > 0 and ph["pass_ms"] > 0
     for r in ph["per_rank"]:  # the phases of one rank sum to at most its solve
         assert r["cand_ms"] + r["xchg_ms"] + r["pass_ms"] <= r["solve_ms"] * 1.001
