@@ -478,25 +478,6 @@ __device__ __forceinline__ void round_keys_init(const RoundKeys &rk, int64_t t) 
   }
 }
 
-// k_csr_keys' per-slot work for slot `slot` of unit `unit` whose candidate
-// list (lane < K: node, -1 = none) is final: bids cleared, the slot's bitmap
-// bit set in the row of every candidate node, the slot opened (or NO_FIT)
-__device__ __forceinline__ void round_keys_slot(const RoundKeys &rk, int32_t slot, int32_t unit,
-                                                int32_t K, int32_t node, int lane) {
-  if (lane < K) {
-    rk.bid[(int64_t)slot * K + lane] = 0xFFFFFFFFu;  // kNoBid
-    // the first bit of a word also sets the word's summary bit
-    if (node >= 0 &&
-        atomicOr(&rk.bm[(int64_t)node * rk.Wb + (slot >> 5)], 1u << (slot & 31)) == 0u)
-      atomicOr(&rk.bms[(int64_t)node * rk.Ws + (slot >> 10)], 1u << ((slot >> 5) & 31));
-  }
-  const int32_t first = __shfl(node, 0, 64);
-  if (lane == 0) {
-    rk.open[slot] = first >= 0 ? 1 : 0;
-    if (first < 0) rk.status[unit] = kNoFit;
-  }
-}
-
 template <template <int> class F, typename... Args>
 int dispatch_D(int D, Args &&...args) {
   switch (D) {

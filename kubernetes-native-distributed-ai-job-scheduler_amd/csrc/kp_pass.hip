@@ -37,18 +37,6 @@
 #ifndef KP_ACC_BIG
 #define KP_ACC_BIG 8  // k_accept of rounds with long bidder rows (kp_ctx::acc_big_ratio)
 #endif
-#ifndef KP_ACC_SPEC
-#define KP_ACC_SPEC 0  // 1: a bidder row's first loads issued before the node's pass flag is known (slower, tools/ab_mix.sh)
-#endif
-#ifndef KP_NREC
-#define KP_NREC 1  // plan pass 0 writes {node, seg_start, seg_end} records for accept
-#endif
-#ifndef KP_ACC_FAST1
-#define KP_ACC_FAST1 1  // one-window bidder rows skip the window-flag step
-#endif
-#ifndef KP_GANG_POST
-#define KP_GANG_POST 0  // >0: no prefetch; the last arriver loads this many parts at once
-#endif
 #ifndef KP_GANG_PRE
 #define KP_GANG_PRE 8  // gang parts prefetched with the arrival ticket (4: +1.4 ms, 8: -0.8 ms vs none)
 #endif
@@ -59,17 +47,11 @@
 #define KP_ACC_WPB 1  // k_accept waves per workgroup (1 vs 4: -0.2 ms per config #3 solve)
 #endif
 static_assert(KP_ACC_WPB >= 1 && KP_ACC_WPB <= 16, "node records carry 16 spare entries");
-#ifndef KP_CSR_PLACE_T
-#define KP_CSR_PLACE_T 1  // k_csr_place_t (candidate-major entry writes); 0: one thread per candidate
-#endif
 #ifndef KP_CSR_PLACE_T_MIN
 #define KP_CSR_PLACE_T_MIN (1 << 20)  // bidder entries from which k_csr_place_t is used
 #endif
 #ifndef KP_ROWS_WPB
 #define KP_ROWS_WPB 16  // k_csr_rows rows (waves) per workgroup
-#endif
-#ifndef KP_ACC_FLAG_FIRST
-#define KP_ACC_FLAG_FIRST 0
 #endif
 
 namespace kp {
@@ -811,16 +793,8 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
   }
 }
 
-#ifndef KP_PLAN_WPE
-#define KP_PLAN_WPE 0  // >0: waves per SIMD the plan's register budget must allow (A/B build knob;
-                       // 7 and 8 measured slower in r05: spills, config #4 +3 / +20 ms)
-#endif
 template <int D, int G, bool W32>
-__global__ __launch_bounds__(64 * KP_PLAN_WPB)
-#if KP_PLAN_WPE > 0
-__attribute__((amdgpu_waves_per_eu(KP_PLAN_WPE, KP_PLAN_WPE)))
-#endif
-void k_plan(PlanArgs pa) {
+__global__ __launch_bounds__(64 * KP_PLAN_WPB) void k_plan(PlanArgs pa) {
   if (pa.pass == 0 && pa.csr_count) {
     // window w = this wave (the grid has >= ceil(A*K/64) waves): the smallest
     // request per dim over its entries, a lower bound for k_accept's pruning
@@ -839,7 +813,7 @@ void k_plan(PlanArgs pa) {
         if ((threadIdx.x & 63) == 0) pa.winmin[(int64_t)d * pa.nwin + w] = (int64_t)x;
       }
     }
-  } else if (KP_NREC && pa.pass == 0) {
+  } else if (pa.pass == 0) {
     // the round's node records {node, seg_start, seg_end}: accept then finds
     // a node's bidder row with its first load (one thread per list entry; the
     // grid has >= A*K >= list-count threads)
@@ -1019,24 +993,8 @@ __device__ __forceinline__ void decide_window(const Win<D, N32> &wc,
       int64_t qq[D];
 #pragma unroll
       for (int d = 0; d < D; ++d) qq[d] = o.q[(int64_t)d * o.U + wc.unit];
-      if (atomicAdd(&o.arrive[wc.slot], 1) + 1 == wc.np) {
-#if KP_GANG_POST > 0
-        // the last arriver loads its gang's parts together (not one per part)
-        int4 post[KP_GANG_POST];
-#pragma unroll
-        for (int i = 0; i < KP_GANG_POST; ++i)
-          post[i] = i < wc.np ? o.gpart[(int64_t)wc.slot * o.K + i] : make_int4(0, 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < KP_GANG_POST; ++i)
-          if (i < wc.np) commit_part<D>(o, wc.lead, post[i], qq);
-        for (int i = KP_GANG_POST; i < wc.np; ++i)
-          commit_part<D>(o, wc.lead, o.gpart[(int64_t)wc.slot * o.K + i], qq);
-        o.status[wc.unit] = kPlaced;
-        close_slot(o, wc.slot);
-#else
+      if (atomicAdd(&o.arrive[wc.slot], 1) + 1 == wc.np)
         commit_gang<D>(o, wc.slot, wc.unit, wc.lead, wc.np, pre, qq);
-#endif
-      }
     }
   }
 }
@@ -1090,10 +1048,8 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
     add[d] = 0;
   }
   const int32_t w0 = e0 >> 6, w1 = (e1 - 1) >> 6;
-#if !KP_ACC_SPEC
   if (nf != pass) return;  // nobody bid on this node in this pass
-#endif
-  if (KP_ACC_FAST1 && w0 == w1) {
+  if (w0 == w1) {  // a one-window row: no window-flag step
     Win<D, N32> wv;
     load_win<D, N32>(wv, w0, lane, e0, e1, pass, ac.P, ac.bid, ac.ent_q, ac.ent_unit,
                           ac.ent_size, ac.ent_lead, ac.ent_slot, ac.s0);
@@ -1184,7 +1140,6 @@ __global__ __launch_bounds__(64 * KP_ACC_WPB) void k_accept(AccArgs ac, int32_t 
     __hip_atomic_store(ac.hflag + pass, ac.htag | (pf ? 1 : 0), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   if (use_list) {  // first record and count loaded together (nrec has 4 spare entries)
-#if KP_NREC
     const int4 r = ac.nrec[wv];
     const int32_t cnt = *ac.nl_count;
     if (wv >= cnt || !pf) return;
@@ -1193,16 +1148,6 @@ __global__ __launch_bounds__(64 * KP_ACC_WPB) void k_accept(AccArgs ac, int32_t 
       const int4 ri = ac.nrec[i];
       accept_node<D, N32, B>(ac, pass, ri.x, ri.y, ri.z);
     }
-#else
-    const int32_t nd = ac.node_list[wv];
-    const int32_t cnt = *ac.nl_count;
-    if (wv >= cnt || !pf) return;
-    accept_node<D, N32, B>(ac, pass, nd, ac.seg_start[nd], ac.seg_end[nd]);
-    for (int i = wv + nw; i < cnt; i += nw) {
-      const int32_t ni = ac.node_list[i];
-      accept_node<D, N32, B>(ac, pass, ni, ac.seg_start[ni], ac.seg_end[ni]);
-    }
-#endif
   } else {
     if (!pf) return;
     for (int node = wv; node < ac.sp.N; node += nw)
@@ -1509,7 +1454,6 @@ int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev) {
                        c->d.counters + 32, c->d.counters + 33);
     KP_HIP(hipGetLastError());
     c->bm_dirty = false;
-#if KP_CSR_PLACE_T
     // large rounds only (config #4: -3 ms per solve); below ~1M entries the
     // one-pass form is faster (config #3 +0.2 ms with the two-phase form)
     if (K <= 1024 && P >= (int64_t)KP_CSR_PLACE_T_MIN) {
@@ -1518,7 +1462,6 @@ int launch_csr_build(kp_ctx *c, int32_t A, int32_t K, const int32_t *A_dev) {
                          c->d.seg_start, c->d.cnt, c->bmin_windows, c->d.rowinfo, c->d.inv,
                          c->d.ent_unit, c->d.ent_slot, c->d.ent_size, c->d.ent_lead, c->d.ent_q);
     } else
-#endif
     hipLaunchKernelGGL(k_csr_place, dim3(blocks(P, 256)), dim3(256), 0, c->stream, A, K, c->D,
                        c->U, Wb, P, A_dev, c->d.cand, c->d.act, c->d.q, c->d.size, c->d.leader,
                        c->d.seg_start, c->d.cnt, c->bmin_windows, c->d.rowinfo, c->d.inv,

@@ -37,6 +37,9 @@
 #include "kp_device.hpp"
 #include "kp_internal.hpp"
 
+// KP_FZ_EXP=1: a measurement-only build (tools/build_variant.sh, the VALU
+// split of tools/gpu_evidence.sh) whose k_score_topk skips the select phase;
+// never the product
 #ifndef KP_FZ_EXP
 #define KP_FZ_EXP 0
 #endif
@@ -63,15 +66,6 @@
   do {                     \
   } while (0)
 #endif
-#ifndef KP_FZ_DMA
-#define KP_FZ_DMA 1  // PRE row records by LDS DMA (0: through VGPRs; A/B knob)
-#endif
-#ifndef KP_FZ_GSURV
-#define KP_FZ_GSURV 1  // survivor scan over the groups whose best reached T (0: the lanes)
-#endif
-#ifndef KP_FZ_FEWSKIP
-#define KP_FZ_FEWSKIP 1  // skip the radix search when fewer than K lane bests are feasible
-#endif
 #ifndef KP_FZ_RANK_UNROLL
 #define KP_FZ_RANK_UNROLL 2  // survivor rank loop unroll (4: +10 ms on config #4, spills)
 #endif
@@ -87,13 +81,7 @@ using namespace dev;
 #define KP_MERGE_WPB 4  // k_merge_tour rows (waves) per workgroup
 #endif
 constexpr int kMergeWPB = KP_MERGE_WPB;
-#ifndef KP_MERGE_KEYS_COMBINE
-#define KP_MERGE_KEYS_COMBINE 1  // one bitmap atomic per (node, candidate index) per merge workgroup
-#endif
-#ifndef KP_MERGE_LOAD_BATCH
-#define KP_MERGE_LOAD_BATCH 8  // k_merge_tour: list loads per lane in flight (1: one 64-key load at a time)
-#endif
-constexpr int kMergeLoadBatch = KP_MERGE_LOAD_BATCH;
+constexpr int kMergeLoadBatch = 8;  // k_merge_tour: list loads per lane in flight
 constexpr int kFzMaxRows = 128;          // rows per workgroup (request stage)
 constexpr int kFzSurv = 128;             // survivor slots per wave (2 per lane)
 // Workgroup shape of k_score_topk: NW waves x 128 columns (2 per lane) =
@@ -222,11 +210,12 @@ void k_score_topk(
   __shared__ __attribute__((aligned(16))) uint64_t sbuf[NW][kFzSurv];
   __shared__ uint32_t spos[NG + NG / 64];   // per group (padded like the tile rows)
   __shared__ uint32_t spos0[NG + NG / 64];  // tie mode 0: the select-phase tie bits
-  __shared__ uint8_t scand[NW][KP_FZ_GSURV ? 64 * GPL : 64];  // per wave: lanes / groups whose best reached T
+  __shared__ uint8_t scand[NW][64 * GPL];  // per wave: the (lane, group) pairs whose best reached T
   constexpr int RW = (2 * D + 4 + 3) & ~3;  // row record words, whole 16-B reads
-  // PRE + KP_FZ_DMA: two buffers, the next chunk's records copied by the
-  // memory unit straight into LDS while the current chunk is scored
-  constexpr int NRB = PRE && KP_FZ_DMA ? 2 : 1;
+  // PRE: two buffers, the next chunk's records copied by the memory unit
+  // straight into LDS while the current chunk is scored (through VGPRs they
+  // spilled at the 80-VGPR budget)
+  constexpr int NRB = PRE ? 2 : 1;
   __shared__ __attribute__((aligned(16))) uint32_t srec[NRB][NW][kFzRC][RW];
   __shared__ int32_t su[PRE ? kFzMaxRows : 1];  // PRE: the rows' units
   auto pgi = [](int g) { return g + (g >> 6); };  // padded group index
@@ -337,7 +326,6 @@ void k_score_topk(
   static_assert(!PRE || kFzRC * Q4 <= 64, "one record piece per lane");
   const int cls = PRE ? tcls[(tile0 >> 7) + wave] : 0;
   const uint4 *crec4 = reinterpret_cast<const uint4 *>(crec);
-#if KP_FZ_DMA
   // rows c .. c + kFzRC - 1 into srec[b][wave]: lane l copies 16-B piece l % Q4
   // of row l / Q4 to byte 16·l of the buffer (the LDS DMA's lane layout)
   auto rec_dma = [&](int c, int b) {
@@ -346,25 +334,13 @@ void k_score_topk(
                                        (void __attribute__((address_space(3))) *)&srec[b][wave][0][0], 16, 0, 0);
   };
   if (PRE) rec_dma(0, 0);
-#else
-  uint4 nx = make_uint4(0u, 0u, 0u, 0u);
-  if (PRE && lane < min(kFzRC, nr) * Q4)
-    nx = crec4[((int64_t)su[lane / Q4] * nfc + cls) * Q4 + lane % Q4];
-#endif
   for (int c0 = 0; c0 < nr; c0 += kFzRC) {
     const int cr = min(kFzRC, nr - c0);
     const int buf = NB == 2 ? (c0 / kFzRC) & 1 : 0;
     const int rb = NRB == 2 ? (c0 / kFzRC) & 1 : 0;
     if constexpr (PRE) {  // 1a. the chunk's row records: one 16-B piece per lane
-#if KP_FZ_DMA
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this chunk's copy has landed
       if (c0 + kFzRC < nr) rec_dma(c0 + kFzRC, rb ^ 1);
-#else
-      if (lane < cr * Q4) reinterpret_cast<uint4 *>(srec[0][wave][lane / Q4])[lane % Q4] = nx;
-      const int c1 = c0 + kFzRC;
-      if (lane < min(kFzRC, nr - c1) * Q4)
-        nx = crec4[((int64_t)su[c1 + lane / Q4] * nfc + cls) * Q4 + lane % Q4];
-#endif
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -527,12 +503,8 @@ void k_score_topk(
       // (strided: the tile's best keys spread over the lanes; the padded rows
       // keep both this pass and the survivor scan free of bank conflicts)
       uint32_t best = 0;
-#if KP_FZ_GSURV
       uint32_t gb[GPL];  // the lane's best key per group
 #pragma unroll
-#else
-#pragma unroll 1
-#endif
       for (int k = 0; k < GPL; ++k) {
         uint32_t v4[4];
         const int gk = pgi(lane + 64 * k);
@@ -545,20 +517,16 @@ void k_score_topk(
           b4 = max(b4, (s1 << ksh) | ((npk - (uint32_t)j * mt) >> rsh));
         }
         best = max(best, b4);
-#if KP_FZ_GSURV
         gb[k] = b4;
-#endif
       }
       // T = the K-th largest lane best (radix select over ballots; lower
       // bound of the tile's K-th key), at least 1 << ksh: every key >= T is
       // feasible
       KP_FZ_PROF_MARK(5);
       uint32_t T = 0;
-#if KP_FZ_FEWSKIP
       // fewer than K lanes with a feasible best: the K-th lane best is below
       // 1 << ksh and T is 1 << ksh without the search (wave-uniform)
       if (__popcll(__ballot(best >= (1u << ksh))) >= K)
-#endif
 #pragma unroll
       for (int bb = 31; bb >= 0; --bb) {
         const uint32_t cb = T | (1u << bb);
@@ -566,7 +534,6 @@ void k_score_topk(
       }
       T = max(T, 1u << ksh);
       KP_FZ_PROF_MARK(6);
-#if KP_FZ_GSURV
       // survivors (keys >= T) -> LDS as exact 64-bit keys. Only the groups
       // whose best reached T hold any (at least K of them, typically about
       // K): their (lane, k) go to LDS in order and the whole wave scans just
@@ -582,19 +549,8 @@ void k_score_topk(
               (uint8_t)(lane | (k << 6));
         m += __popcll(Mk);
       }
-      constexpr int CPL = 4;  // columns per listed entry
-#else
-      // survivors (keys >= T) -> LDS as exact 64-bit keys. Only lanes whose
-      // best reached T hold any (at least K of them): their lane numbers go
-      // to LDS in order and the whole wave scans just their 16 columns each
-      const uint64_t M = __ballot(best >= T);
-      const int m = __popcll(M);
-      if (best >= T)
-        scand[wave][__builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
-                                              __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u))] =
-            (uint8_t)lane;
-      constexpr int CPL = 4 * GPL;  // columns per lane
-#endif
+      constexpr int CPL = 4;        // columns per listed entry
+      constexpr int CPB = 4 * GPL;  // columns per lane (the bisection re-reads them all)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -605,13 +561,8 @@ void k_score_topk(
         bool hit = false;
         uint32_t s1 = 0, ntk = 0;
         if (e < CPL * m) {
-#if KP_FZ_GSURV
           const int ent = scand[wave][e >> 2];  // listed (lane, group k)
           const int g = pgi((ent & 63) + 64 * (ent >> 6)), jj = e & 3;
-#else
-          const int L = scand[wave][e / CPL];          // candidate lane
-          const int g = pgi(L + 64 * ((e >> 2) & (GPL - 1))), jj = e & 3;  // its column group, column
-#endif
           s1 = load_one<H16>(srow, 4 * g + jj);
           ntk = nsl - spos[g] - (uint32_t)jj * mul;
           hit = ((s1 << ksh) | ((nst - tsp[g] - (uint32_t)jj * mt) >> rsh)) >= T;
@@ -631,7 +582,7 @@ void k_score_topk(
           const uint64_t cb = pre | (1ull << bb);
           int c = 0;
 #pragma unroll 1
-          for (int e = 0; e < CPL; ++e) {
+          for (int e = 0; e < CPB; ++e) {
             const int k = e >> 2, j = e & 3;
             const uint32_t s1 = load_one<H16>(srow, 4 * pgi(lane + 64 * k) + j);
             const uint32_t ntk = nsl - spos[pgi(lane + 64 * k)] - (uint32_t)j * mul;
@@ -642,7 +593,7 @@ void k_score_topk(
         }
         C = 0;
 #pragma unroll 1
-        for (int e = 0; e < CPL; ++e) {
+        for (int e = 0; e < CPB; ++e) {
           const int k = e >> 2, j = e & 3;
           const uint32_t s1 = load_one<H16>(srow, 4 * pgi(lane + 64 * k) + j);
           const uint32_t ntk = nsl - spos[pgi(lane + 64 * k)] - (uint32_t)j * mul;
@@ -766,9 +717,6 @@ __global__ __launch_bounds__(64 * KP_MERGE_WPB) void k_merge_tour(ScoreParams sp
   }
   const int row = blockIdx.x * kMergeWPB + wave;
   const bool live = row < rows && !(rows_dev && row >= *rows_dev);  // wave-uniform
-#if !KP_MERGE_KEYS_COMBINE
-  if (!live) return;  // no barrier below
-#endif
   const int K = sp.n_cand, M = ntiles * K;
   int32_t unit = 0, mine = -1;
   if (live) {
@@ -800,7 +748,6 @@ __global__ __launch_bounds__(64 * KP_MERGE_WPB) void k_merge_tour(ScoreParams sp
     mine = (uint32_t)mypos < (uint32_t)sp.N ? perm[mypos] : -1;
     if (lane < K) cand[(int64_t)row * K + lane] = mine;
   }
-#if KP_MERGE_KEYS_COMBINE
   if (rk.enabled) {  // k_csr_keys' work for the workgroup's slots
     // the slots of a workgroup share one bitmap word (kMergeWPB divides 32):
     // the first wave with node n at candidate index j sets the bits of every
@@ -833,9 +780,6 @@ __global__ __launch_bounds__(64 * KP_MERGE_WPB) void k_merge_tour(ScoreParams sp
       }
     }
   }
-#else
-  if (rk.enabled) round_keys_slot(rk, row, unit, K, mine, lane);  // k_csr_keys' work for the slot
-#endif
 }
 
 template <int D>

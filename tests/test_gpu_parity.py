@@ -1021,6 +1021,29 @@ def test_fused_key_collisions(oracle, monkeypatch, tie, bits, K):
     _assert_same(g, o, f"collisions tie={tie} bits={bits} K={K}")
 
 
+@pytest.mark.parametrize("tie", [0, 1])
+@pytest.mark.parametrize("K", [4, 16, 32])
+def test_fused_bisection_all_ties(oracle, monkeypatch, tie, K):
+    """Every column of every tile ties on score (identical empty nodes, one
+    request shape) and the select keys keep one tie bit (KP_FZ_TIE_BITS=1):
+    about half of each tile's 1,024 columns reach T, far past the 128
+    survivor slots, so every row takes the exact 64-bit bisection, which
+    must re-read all 16 columns of each lane (4-column groups L + 64k)."""
+    monkeypatch.setenv("KP_FZ_TIE_BITS", "1")
+    N, J = 3000, 700
+    cap = np.ascontiguousarray(np.tile(np.array([[64000], [524288], [8], [8 * 294912]], np.int64), (1, N)))
+    req = np.ascontiguousarray(np.tile(np.array([[1000], [1024], [1], [16384]], np.int64), (1, J)))
+    w = synth.Workload(J, N, 4, req, cap, np.zeros_like(cap), np.zeros(J, np.int32),
+                       np.full(J, -1, np.int32), np.ones(J, np.int32),
+                       (np.arange(N) // 32).astype(np.int32), name="ties")
+    p = _abi.default_params(tie_mode=tie, n_cand=K, w_spread=0)
+    with Placer(device=0) as pl:
+        g = pl.place(w, p)
+        assert pl.timing()["fused"] == 1
+    o = oracle.place(_snap(oracle, w), p, nthreads=NTH)
+    _assert_same(g, o, f"all ties tie={tie} K={K}")
+
+
 # ---------------------------------------------------------------------------
 # the product is the default path: knobs need the gate, fixtures hold on the GPU
 # ---------------------------------------------------------------------------

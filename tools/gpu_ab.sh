@@ -3,7 +3,7 @@
 # libkplace.so): config #3 solve (tools/cfg_time.py) alternated x3, then the
 # config #4 solve (tools/c4_time.py) alternated x2. LIBS overrides the list.
 set -o pipefail
-OUT=gpurun_out/ab_libs; mkdir -p $OUT
+OUT=${OUT:-gpurun_out/ab_libs}; mkdir -p $OUT
 LIBS=${LIBS:-"base cur"}
 lib_of() { [ "$1" = cur ] && echo "$PWD/kubernetes-native-distributed-ai-job-scheduler_amd/libkplace.so" || echo "$PWD/abl/$1.so"; }
 for i in 1 2 3; do for l in $LIBS; do
