@@ -508,7 +508,7 @@ def main():
                     help="config #4 CPU baseline sample: the first N pending jobs")
     ap.add_argument("--cpu-c4-rounds", type=int, default=3,
                     help="config #4 CPU baseline sample: rounds of their solve")
-    ap.add_argument("--cpu-c4-preemptors", type=int, default=2_000,
+    ap.add_argument("--cpu-c4-preemptors", type=int, default=10_000,
                     help="config #4 CPU preemption sample: the first N of the GPU leg's preemptors")
     ap.add_argument("--c2-jobs", type=int, default=10_000)
     ap.add_argument("--c2-nodes", type=int, default=1_000)
