@@ -45,6 +45,7 @@ import argparse
 import json
 import os
 import platform
+import re
 import subprocess
 import sys
 import time
@@ -66,6 +67,13 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 # SIMD issue ~56 T lane-ops/s (tools/valu_peak.hip, profiles/r05_valu_peak.txt:
 # 32 lanes per clock at the ~1.7 GHz the chip holds under that load)
 VALU_ACHIEVABLE_TOPS = 56.4
+
+
+def newest(kind: str) -> list:
+    """profiles/rNN_<kind>.json, newest round first (the evidence the line cites)."""
+    d = os.path.join(REPO, "profiles")
+    names = [n for n in os.listdir(d) if re.fullmatch(r"r\d\d_" + kind + r"\.json", n)] if os.path.isdir(d) else []
+    return sorted(names, reverse=True)
 
 
 def progress(msg: str) -> None:
@@ -438,7 +446,7 @@ def score_matrix(args, make_placer, w, p, rank=0, world=1, gather=lambda d: [d])
     pairs = float(w.J) * w.N * args.score_steps
     kname = "k_score32c" if tm["score_form"] == 1 else "k_score32"
     traffic, traffic_src = None, None
-    for pmc in ("r05_pmc.json", "r04_pmc.json"):  # HBM-side bytes per launch (rocprofv3 PMC), newest first
+    for pmc in newest("pmc"):  # HBM-side bytes per launch (rocprofv3 PMC), newest first
         path = os.path.join(REPO, "profiles", pmc)
         if os.path.exists(path):
             with open(path) as f:
@@ -672,7 +680,7 @@ def main():
     fused = bool(tm["fused"])
     kname = "k_score_topk" if fused else "k_score32"
     traffic, traffic_src, valu = None, None, None
-    for pmc in ("r05_pmc.json", "r04_pmc.json", "r03_pmc.json", "r02_pmc.json", "r01_pmc.json"):  # HBM-side bytes per launch (rocprofv3 PMC), newest first
+    for pmc in newest("pmc"):  # HBM-side bytes per launch (rocprofv3 PMC), newest first
         path = os.path.join(REPO, "profiles", pmc)
         if os.path.exists(path):
             with open(path) as f:
@@ -687,7 +695,7 @@ def main():
         # judged on pairs/s and on the VALU roofline (lane-ops per pair from
         # the SQ_INSTS_VALU counter of the same solve, profiles/r0N_valu.json)
         opp, vsrc = None, None
-        for vj in ("r05_valu.json", "r04_valu.json", "r03_valu.json", "r02_valu.json"):  # newest evidence first
+        for vj in newest("valu"):  # newest evidence first
             path = os.path.join(REPO, "profiles", vj)
             if os.path.exists(path):
                 with open(path) as f:

@@ -613,7 +613,7 @@ __device__ __forceinline__ int32_t in_vgpr(int32_t s) {
 }
 
 template <int D, bool MOST, bool WS, bool WM>
-__global__ __launch_bounds__(256) void k_score32c(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 6))) void k_score32c(
     ScoreParams sp, const uint32_t *__restrict__ np, int32_t P, const int64_t *__restrict__ q,
     int32_t qstride, const int32_t *__restrict__ uaff, const int32_t *__restrict__ rows_unit,
     int32_t rows, int32_t rows_per_block, int32_t min_rpb, int32_t *__restrict__ score,
@@ -730,35 +730,67 @@ __global__ __launch_bounds__(256) void k_score32c(
       }
     }
     int32_t *srow = WS ? score + (int64_t)r * sstride + tile0 : nullptr;  // wave-uniform
-    uint64_t word[NC];
-#pragma unroll
-    for (int k = 0; k < NC; ++k) {
-      bool ft = v_[k];
-      int32_t acc = wa_[k] + (int32_t)x[k][D];
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        ft &= qq[d] <= f_[k][d];
-        acc += a_[k][d] >= x[k][d] ? w_[d] : 0;
-      }
-      // GPU-topology fit (the job takes exactly the node's free GPUs) and the
-      // CacheStrategy=shared affinity domain
-      const int32_t bonus = (fg_[k] == qg ? wfit_r : 0) + (tp_[k] == af ? waff : 0);
-      const int32_t sc = (MOST ? acc : b_[k] - acc) + bonus;
-      // the ballot in the block of the compares (across the store's branch
-      // the compiler re-materialises the mask through a VGPR)
-      word[k] = __ballot(ft);  // columns tile0 + 64k .. + 63: mask word (tile0 >> 6) + k
-      // the matrix is streamed out once: non-temporal stores (1.10-1.14 ->
-      // 1.01-1.04 ms per config #3 call; the mask's 32-B pieces stay cached)
-      if (WS && k < nk) __builtin_nontemporal_store(ft ? sc : KP_SCORE_INFEASIBLE, srow + 64 * k + lane);
-    }
-    if (WM) {  // lane k < nk stores word k (scalar values written into lanes)
-      uint32_t lo = 0u, hi = 0u;
+    // FULL: all NC column groups inside the row stride (every wave but the
+    // last tile's), so the stores need no guard and the ballots stay in
+    // SGPRs (a guarded store made the compiler re-materialise each mask
+    // through a VGPR); HG / HA: the row has a GPU request / an affinity
+    // domain — rows without skip those compares (scalar branches: qg and af
+    // are SGPR values)
+    auto body = [&](auto full_, auto hg_, auto ha_) {
+      constexpr bool FULL = decltype(full_)::value, HG = decltype(hg_)::value,
+                     HA = decltype(ha_)::value;
+      uint64_t word[NC];
 #pragma unroll
       for (int k = 0; k < NC; ++k) {
-        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(lo) : "s"((uint32_t)word[k]), "n"(k));
-        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(hi) : "s"((uint32_t)(word[k] >> 32)), "n"(k));
+        bool ft = v_[k];
+        int32_t acc = wa_[k] + (int32_t)x[k][D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          ft &= qq[d] <= f_[k][d];
+          acc += a_[k][d] >= x[k][d] ? w_[d] : 0;
+        }
+        // GPU-topology fit (the job takes exactly the node's free GPUs) and
+        // the CacheStrategy=shared affinity domain
+        int32_t bonus = 0;
+        if constexpr (HG) bonus += fg_[k] == qg ? wfit_r : 0;
+        if constexpr (HA) bonus += tp_[k] == af ? waff : 0;
+        const int32_t sc = (MOST ? acc : b_[k] - acc) + bonus;
+        word[k] = __ballot(ft);  // columns tile0 + 64k .. + 63: mask word (tile0 >> 6) + k
+        // the matrix is streamed out once: non-temporal stores (1.10-1.14 ->
+        // 1.01-1.04 ms per config #3 call; the mask's 32-B pieces stay cached)
+        if (WS && (FULL || k < nk)) __builtin_nontemporal_store(ft ? sc : KP_SCORE_INFEASIBLE, srow + 64 * k + lane);
       }
-      if (lane < nk) mask[(int64_t)r * mstride + (tile0 >> 6) + lane] = ((uint64_t)hi << 32) | lo;
+      if (WM) {  // lane k < nk stores word k (scalar values written into lanes), in
+                 // the variant's own block: the masks never leave their SGPRs
+        // one asm block led by s_nop 4: the compiler's hazard recognizer
+        // does not look inside inline asm, and a ballot's SGPRs written by
+        // the VALU just before a v_writelane reads them came out stale
+        static_assert(NC == 4, "the writelane block below covers 4 words");
+        uint32_t lo = 0u, hi = 0u;
+        asm volatile(
+            "s_nop 4\n\t"
+            "v_writelane_b32 %0, %2, 0\n\tv_writelane_b32 %1, %3, 0\n\t"
+            "v_writelane_b32 %0, %4, 1\n\tv_writelane_b32 %1, %5, 1\n\t"
+            "v_writelane_b32 %0, %6, 2\n\tv_writelane_b32 %1, %7, 2\n\t"
+            "v_writelane_b32 %0, %8, 3\n\tv_writelane_b32 %1, %9, 3"
+            : "+v"(lo), "+v"(hi)
+            : "s"((uint32_t)word[0]), "s"((uint32_t)(word[0] >> 32)), "s"((uint32_t)word[1]),
+              "s"((uint32_t)(word[1] >> 32)), "s"((uint32_t)word[2]), "s"((uint32_t)(word[2] >> 32)),
+              "s"((uint32_t)word[3]), "s"((uint32_t)(word[3] >> 32)));
+        if (lane < nk) mask[(int64_t)r * mstride + (tile0 >> 6) + lane] = ((uint64_t)hi << 32) | lo;
+      }
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    const bool hg = wfit_r != 0, ha = (int32_t)af >= 0;
+    if (nk == NC) {
+      if (hg) {
+        if (ha) body(T_{}, T_{}, T_{}); else body(T_{}, T_{}, F_{});
+      } else {
+        if (ha) body(T_{}, F_{}, T_{}); else body(T_{}, F_{}, F_{});
+      }
+    } else {
+      body(F_{}, T_{}, T_{});
     }
   }
 }

@@ -61,8 +61,8 @@ if [ "$SKIP_C4" != 1 ]; then
   SUFFIX=_ev bash tools/gpu_c4_trace.sh > $OUT/c4_trace.log 2>&1 || { tail -5 $OUT/c4_trace.log; exit 1; }
   echo c4 ok
 fi
-python3 tools/evidence_summary.py ${ROUND:-r05} $OUT $OUT/summary && ls $OUT/summary
-R=${ROUND:-r05}
+python3 tools/evidence_summary.py ${ROUND:-r06} $OUT $OUT/summary && ls $OUT/summary
+R=${ROUND:-r06}
 if [ -f gpurun_out/c4_profile/summary.txt ]; then cp gpurun_out/c4_profile/summary.txt $OUT/summary/${R}_c4_profile.txt; fi
 if [ -f gpurun_out/c4t_ev/pass_sum.txt ]; then
   { echo "# config #4 kernel trace of tools/c4_time.py (rocprofv3 --kernel-trace): per pass index, summed / largest k_accept and k_plan launch (tools/pass_trace_sum.py); then per-round kernel times (tools/round_kernel_sum.py)"
