@@ -22,15 +22,15 @@ if [ "$SKIP_BENCH" != 1 ]; then
   echo bench ok
 fi
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-B3="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-stream --no-config4 --place-steps 0 --no-score-matrix --no-phases"
+B3="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-stream --no-config4 --no-config2 --place-steps 0 --no-score-matrix --no-phases"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $B3 --out $OUT/prof/bench_prof.json > $OUT/prof/bench.log 2>&1 || exit $?
 echo prof ok
 # the materialised score matrix + mask (kp_score_dev, config #3 full queue) on its own
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsm -o run -- python3 tools/score_dev_time.py > $OUT/profsm/score_dev.log 2>&1 || exit $?
 echo profsm ok
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof45 -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --place-steps 0 --c4-steps 1 --no-phases --out $OUT/prof45/bench_prof.json > $OUT/prof45/bench.log 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof45 -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-config2 --place-steps 0 --c4-steps 1 --no-phases --out $OUT/prof45/bench_prof.json > $OUT/prof45/bench.log 2>&1 || exit $?
 echo prof45 ok
-B1="bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-stream --no-config4 --place-steps 0 --no-phases"
+B1="bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-stream --no-config4 --no-config2 --place-steps 0 --no-phases"
 RE='k_score|k_select|k_merge|k_plan|k_accept'
 pmc() {  # name, counters...
   local n=$1; shift
