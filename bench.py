@@ -522,7 +522,7 @@ def main():
     ap.add_argument("--c2-nodes", type=int, default=1_000)
     ap.add_argument("--c2-steps", type=int, default=20)
     ap.add_argument("--no-config2", action="store_true")
-    ap.add_argument("--cpu-stream-batches", type=int, default=4,
+    ap.add_argument("--cpu-stream-batches", type=int, default=8,
                     help="config #5 CPU baseline sample: the first N micro-batches")
     ap.add_argument("--no-phases", action="store_true",
                     help="skip the extra solve with per-round phase events (profiling runs that count "
