@@ -502,37 +502,53 @@ void k_score_topk(
       // lane L's 16 columns are the 4-column groups L + 64k, k < GPL
       // (strided: the tile's best keys spread over the lanes; the padded rows
       // keep both this pass and the survivor scan free of bank conflicts)
+      // 16-bit scores: the select key is (s + 1) << 16 | the top 16 tie
+      // bits, built from the packed LDS word by one v_alignbit (low column)
+      // or v_perm (high column) per column; tests with fewer tie bits
+      // (KP_FZ_TIE_BITS < 16) mask the low key bits per group (max commutes
+      // with the mask). 32-bit scores: (s + 1) << ksh | tie >> rsh
+      const int kss = H16 ? 16 : ksh;
+      const uint32_t kmask = H16 && tbits < 16 ? ~((1u << (16 - tbits)) - 1u) : 0xFFFFFFFFu;
+      auto key32 = [&](uint32_t s1, uint32_t tk) {
+        return H16 ? (((s1 << 16) | (tk >> 16)) & kmask) : ((s1 << ksh) | (tk >> rsh));
+      };
       uint32_t best = 0;
       uint32_t gb[GPL];  // the lane's best key per group
 #pragma unroll
       for (int k = 0; k < GPL; ++k) {
-        uint32_t v4[4];
         const int gk = pgi(lane + 64 * k);
-        load_group<H16>(ssc[buf][i], gk, v4);
         const uint32_t npk = nst - tsp[gk];
         uint32_t b4 = 0;
+        if constexpr (H16) {
+          const uint2 x = reinterpret_cast<const uint2 *>(ssc[buf][i])[gk];
+          const uint32_t k0 = __builtin_amdgcn_alignbit(x.x, npk, 16);
+          const uint32_t k1 = __builtin_amdgcn_perm(x.x, npk - mt, 0x07060302u);
+          const uint32_t k2 = __builtin_amdgcn_alignbit(x.y, npk - 2u * mt, 16);
+          const uint32_t k3 = __builtin_amdgcn_perm(x.y, npk - 3u * mt, 0x07060302u);
+          b4 = max(max(k0, k1), max(k2, k3)) & kmask;
+        } else {
+          uint32_t v4[4];
+          load_group<H16>(ssc[buf][i], gk, v4);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t s1 = v4[j];
-          b4 = max(b4, (s1 << ksh) | ((npk - (uint32_t)j * mt) >> rsh));
+          for (int j = 0; j < 4; ++j) b4 = max(b4, key32(v4[j], npk - (uint32_t)j * mt));
         }
         best = max(best, b4);
         gb[k] = b4;
       }
       // T = the K-th largest lane best (radix select over ballots; lower
-      // bound of the tile's K-th key), at least 1 << ksh: every key >= T is
+      // bound of the tile's K-th key), at least 1 << kss: every key >= T is
       // feasible
       KP_FZ_PROF_MARK(5);
       uint32_t T = 0;
       // fewer than K lanes with a feasible best: the K-th lane best is below
-      // 1 << ksh and T is 1 << ksh without the search (wave-uniform)
-      if (__popcll(__ballot(best >= (1u << ksh))) >= K)
+      // 1 << kss and T is 1 << kss without the search (wave-uniform)
+      if (__popcll(__ballot(best >= (1u << kss))) >= K)
 #pragma unroll
       for (int bb = 31; bb >= 0; --bb) {
         const uint32_t cb = T | (1u << bb);
         T = __popcll(__ballot(best >= cb)) >= K ? cb : T;
       }
-      T = max(T, 1u << ksh);
+      T = max(T, 1u << kss);
       KP_FZ_PROF_MARK(6);
       // survivors (keys >= T) -> LDS as exact 64-bit keys. Only the groups
       // whose best reached T hold any (at least K of them, typically about
@@ -565,7 +581,7 @@ void k_score_topk(
           const int g = pgi((ent & 63) + 64 * (ent >> 6)), jj = e & 3;
           s1 = load_one<H16>(srow, 4 * g + jj);
           ntk = nsl - spos[g] - (uint32_t)jj * mul;
-          hit = ((s1 << ksh) | ((nst - tsp[g] - (uint32_t)jj * mt) >> rsh)) >= T;
+          hit = key32(s1, nst - tsp[g] - (uint32_t)jj * mt) >= T;
         }
         const uint64_t mm = __ballot(hit);
         const int p = C + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32),
