@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "kp_internal.hpp"
 
@@ -407,6 +408,24 @@ __device__ __forceinline__ uint32_t group_max_u32(uint32_t v) {
     const uint32_t r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
     if constexpr (G == 32) return lane_id() < 32 ? max(r0, r1) : max(r2, r3);
     return max(max(r0, r1), max(r2, r3));
+  }
+}
+
+// A loaded value that must be in a register here: an empty asm reads it
+// (and hands it back opaque, so nothing computed from it moves above this
+// point). Put after a group of independent loads, it makes the compiler issue
+// them all before its one wait. Without it the latency-bound pass kernels had
+// loads sunk below the first branch that did not need them, or waited for
+// early by arithmetic hoisted above a branch: one dependent memory level each.
+template <typename T>
+__device__ __forceinline__ void landed(T &v) {
+  static_assert(std::is_arithmetic<T>::value, "a scalar value (one component of a vector load)");
+  if constexpr (sizeof(T) < 4) {
+    uint32_t t = (uint32_t)v;
+    asm volatile("" : "+v"(t));
+    v = (T)t;
+  } else {
+    asm volatile("" : "+v"(v));
   }
 }
 

@@ -228,7 +228,7 @@ struct kp_ctx {
   // score launch geometry (tuning knobs): target workgroups per launch and
   // the smallest number of job rows per workgroup
   int32_t score_wg_target = 4096, score_min_rpb = 4, score_npl = 2;
-  int32_t fz_wg_target = 2048;  // KP_FZ_WG_TARGET: target workgroups of k_score_topk
+  int32_t fz_wg_target = 4096;  // KP_FZ_WG_TARGET: target workgroups of k_score_topk (r06: 2048 -> 4096, config #3 -2.7 %)
   bool fz_h16 = true;     // KP_FZ_H16=0: 32-bit LDS scores in k_score_topk
   int32_t fz_tie_bits = 0;  // KP_FZ_TIE_BITS=b (tests): b select-phase tie bits, forces collisions
   // KP_ACC_WAVES: largest k_accept grid in waves, grid-stride over the rest (0 =

@@ -529,14 +529,25 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
   const int a = wave_global * SPW + lane / G;
   const int K = sp.n_cand, N = sp.N, U = pa.U;
   const int aa = min(a, pa.A - 1);  // host bound A > 0
-  const uint8_t op = pa.open[aa];
-  const int32_t u0 = pa.act[aa];
-  const int32_t node = gl < K ? pa.cand[(int64_t)aa * K + gl] : -1;
+  const int gk = min(gl, K - 1);     // in bounds: the loads need no lane mask
+  uint8_t op = pa.open[aa];
+  int32_t u0 = pa.act[aa];
+  int32_t node_raw = pa.cand[(int64_t)aa * K + gk];
+  int32_t inv_ld = pa.inv[(int64_t)aa * K + gk];
+  int32_t prev = pass > 0 ? pa.pass_flag[pass - 1] : 1;
+  int32_t adev = pa.A_dev ? *pa.A_dev : pa.A;
+  // the first memory level: one wait for all of it
+  landed(op);
+  landed(u0);
+  landed(node_raw);
+  landed(inv_ld);
+  landed(prev);
+  landed(adev);
+  const int32_t node = gl < K ? node_raw : -1;
   // valid iff node >= 0; bit 31: the entry's bidder row is long (k_csr_place)
-  const int32_t inv_raw = gl < K ? pa.inv[(int64_t)aa * K + gl] : 0;
+  const int32_t inv_raw = gl < K ? inv_ld : 0;
   const int32_t e_inv = inv_raw & 0x7FFFFFFF;
-  const int32_t prev = pass > 0 ? pa.pass_flag[pass - 1] : 1;
-  const int32_t A = pa.A_dev ? min(pa.A, *pa.A_dev) : pa.A;
+  const int32_t A = min(pa.A, adev);
   // a pass after one without proposals has none either (usage unchanged,
   // open slots only close): the round is over
   if (!prev) return;
@@ -545,14 +556,20 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
   KP_PP_MARK(0);
   if (__ballot(slot_ok) == 0) return;
   KP_PP_WORK();
+  // the second memory level (the unit's request, the candidate's record and
+  // usage): unconditional loads at valid indices, one wait for all of them
   const int32_t u = slot_ok ? u0 : 0;
-  const int32_t sz = slot_ok ? pa.size[u] : 0;
-  const int32_t af = slot_ok ? pa.aff[u] : -1;
+  int32_t sz_ld = pa.size[u], af_ld = pa.aff[u];
   int64_t qq[D];
 #pragma unroll
-  for (int d = 0; d < D; ++d) qq[d] = slot_ok ? pa.q[(int64_t)d * U + u] : 0;
+  for (int d = 0; d < D; ++d) qq[d] = pa.q[(int64_t)d * U + u];
   const bool valid = slot_ok && node >= 0;
   const int nn = valid ? node : 0;
+  uint32_t used32[D];
+  if constexpr (W32) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) used32[d] = (uint32_t)pa.used[(int64_t)d * N + nn];
+  }
   int32_t planned = 0, dom = 0, s0 = -1;
   bool fail = !slot_ok;
   // this lane's candidate node: the static operands of the W32 loop come as
@@ -562,7 +579,18 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
   int32_t nbase = 0, tp;
   if constexpr (REC) {
     const uint4 *rec = reinterpret_cast<const uint4 *>(pa.nst) + (int64_t)nn * 4;
-    const uint4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
+    uint4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
+    landed(r0.x);  // one component waits for the whole 16-B load
+    landed(r1.x);
+    landed(r2.x);
+    landed(r3.x);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      landed(qq[d]);
+      landed(used32[d]);
+    }
+    landed(sz_ld);
+    landed(af_ld);
     const uint32_t c4[4] = {r0.x, r0.y, r0.z, r0.w}, R4[4] = {r1.x, r1.y, r1.z, r1.w},
                    K4[4] = {r2.x, r2.y, r2.z, r2.w};
 #pragma unroll
@@ -576,6 +604,10 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
   } else {
     tp = pa.topo[nn];
   }
+  const int32_t sz = slot_ok ? sz_ld : 0;
+  const int32_t af = slot_ok ? af_ld : -1;
+#pragma unroll
+  for (int d = 0; d < D; ++d) qq[d] = slot_ok ? qq[d] : 0;
   int32_t szmax = sz;
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) szmax = max(szmax, __shfl_xor(szmax, m, kWave));
@@ -591,7 +623,7 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       q32[d] = (uint32_t)qq[d];
-      const uint32_t uu = (uint32_t)pa.used[(int64_t)d * N + nn];
+      const uint32_t uu = used32[d];
       const uint32_t cc = REC ? ncap[d] : (uint32_t)pa.cap[(int64_t)d * N + nn];
       const uint32_t rr = REC ? nR[d] : pa.R32[(int64_t)d * N + nn];
       const uint32_t kk = REC ? nK[d] : pa.K32[(int64_t)d * N + nn];
@@ -840,8 +872,15 @@ struct Win {
   using NT = typename std::conditional<N32, uint32_t, int64_t>::type;
   int32_t e, m, np, unit, size, lead, slot, s0;
   NT need[D];
+  // raw loads, turned into m / np / need by finish_win once they have landed
+  uint32_t t;
+  int64_t qd[D];
+  bool in_row;
 };
 
+// the loads of a window's entries (all issued together; nothing is computed
+// from them here, so they land in one memory level with whatever the caller
+// issues next)
 template <int D, bool N32>
 __device__ __forceinline__ void load_win(Win<D, N32> &w, int wi, int lane, int32_t e0, int32_t e1,
                                          int32_t pass, int64_t P,
@@ -852,28 +891,44 @@ __device__ __forceinline__ void load_win(Win<D, N32> &w, int wi, int lane, int32
                                          const int32_t *__restrict__ ent_lead,
                                          const int32_t *__restrict__ ent_slot,
                                          const int32_t *__restrict__ s0) {
+  (void)pass;
   w.e = (wi << 6) + lane;
-  w.m = 0;
-  w.np = 0;
-  const bool in_row = wi >= 0 && w.e >= e0 && w.e < e1;
-  const int32_t ee = in_row ? w.e : e0;
-  const uint32_t t = bid[ee];
+  w.in_row = wi >= 0 && w.e >= e0 && w.e < e1;
+  const int32_t ee = w.in_row ? w.e : e0;
+  w.t = bid[ee];
   w.unit = ent_unit[ee];
   w.size = ent_size[ee];
   w.lead = ent_lead[ee];
   w.slot = ent_slot[ee];
   w.s0 = s0[ee];
-  int64_t qd[D];
 #pragma unroll
-  for (int d = 0; d < D; ++d) qd[d] = ent_q[(int64_t)d * P + ee];
-  if (in_row && (t >> 16) == (uint32_t)pass) {
-    w.m = (int32_t)(t & 0xFFu);
-    w.np = (int32_t)((t >> 8) & 0xFFu);
+  for (int d = 0; d < D; ++d) w.qd[d] = ent_q[(int64_t)d * P + ee];
+}
+
+template <int D, bool N32>
+__device__ __forceinline__ void landed_win(Win<D, N32> &w) {
+  landed(w.t);
+  landed(w.unit);
+  landed(w.size);
+  landed(w.lead);
+  landed(w.slot);
+  landed(w.s0);
+#pragma unroll
+  for (int d = 0; d < D; ++d) landed(w.qd[d]);
+}
+
+template <int D, bool N32>
+__device__ __forceinline__ void finish_win(Win<D, N32> &w, int32_t pass) {
+  w.m = 0;
+  w.np = 0;
+  if (w.in_row && (w.t >> 16) == (uint32_t)pass) {
+    w.m = (int32_t)(w.t & 0xFFu);
+    w.np = (int32_t)((w.t >> 8) & 0xFFu);
   }
   // a bid's members fit the node at plan time: m·q <= cap (< 2^26 with N32)
 #pragma unroll
   for (int d = 0; d < D; ++d)
-    w.need[d] = w.m > 0 ? (typename Win<D, N32>::NT)((int64_t)w.m * qd[d]) : 0;
+    w.need[d] = w.m > 0 ? (typename Win<D, N32>::NT)((int64_t)w.m * w.qd[d]) : 0;
 }
 
 struct AcceptOut {
@@ -1040,25 +1095,48 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
   KP_PP_DECL(ac.pp, 16, ac.pp ? (int)(ac.st->rounds - 1) * 16 + pass : 1024);
 #endif
   if (e0 < 0) return;  // no bidder row this round
-  const int32_t nf = ac.node_flag[node];
+  int32_t nf = 0;
   NT rem[D], add[D];
+  int64_t ncap[D], nused[D];
 #pragma unroll
-  for (int d = 0; d < D; ++d) {
-    rem[d] = (NT)(ac.cap[(int64_t)d * N + node] - o.used[(int64_t)d * N + node]);
-    add[d] = 0;
-  }
+  for (int d = 0; d < D; ++d) add[d] = 0;
+  // the node's flag and operands: issued inside each path below, after its
+  // branch, and landed together with the path's first window loads (issued
+  // before the branch, the path's entry waited for them)
+  auto node_load = [&]() {
+    nf = ac.node_flag[node];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      ncap[d] = ac.cap[(int64_t)d * N + node];
+      nused[d] = o.used[(int64_t)d * N + node];
+    }
+  };
+  auto node_landed = [&]() {
+    landed(nf);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      landed(ncap[d]);
+      landed(nused[d]);
+      rem[d] = (NT)(ncap[d] - nused[d]);
+    }
+  };
   const int32_t w0 = e0 >> 6, w1 = (e1 - 1) >> 6;
-  if (nf != pass) return;  // nobody bid on this node in this pass
   if (w0 == w1) {  // a one-window row: no window-flag step
     Win<D, N32> wv;
     load_win<D, N32>(wv, w0, lane, e0, e1, pass, ac.P, ac.bid, ac.ent_q, ac.ent_unit,
                           ac.ent_size, ac.ent_lead, ac.ent_slot, ac.s0);
+    node_load();
+    // the node's flag and operands and the window: one memory level
+    landed_win(wv);
+    node_landed();
+    finish_win(wv, pass);
     KP_PP_MARK(0);
     if (nf != pass) return;  // nobody bid on this node in this pass
     KP_PP_WORK();
     decide_window<D, N32>(wv, rem, add, lane, node, o);
     KP_PP_MARK(3);
   } else {
+    node_load();
     constexpr int BATCH = B;  // flagged windows whose operands are loaded together
     for (int wb = w0; wb <= w1; wb += 64) {
       const int wi = wb + lane;
@@ -1069,13 +1147,21 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
       const bool lrow = w1 - w0 + 1 >= ac.bmin_windows;  // wave-uniform, as k_csr_place
       int64_t wmin[D];
       uint64_t braw[D];
+      int32_t wf = -1;
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         wmin[d] = mine ? ac.winmin[(int64_t)d * ac.nwin + wi] : 0;
         braw[d] = mine && lrow ? (uint64_t)ac.bmin[(int64_t)d * ac.nwin + wi] : 0;
       }
-      const int32_t wf = mine ? ac.win[wi] : -1;
+      wf = mine ? ac.win[wi] : -1;
       if (wb == w0) {  // the first chunk's flags were loaded with the node's operands
+        node_landed();
+        landed(wf);
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          landed(wmin[d]);
+          landed(braw[d]);
+        }
         KP_PP_MARK(0);
         if (nf != pass) return;
         KP_PP_WORK();
@@ -1108,6 +1194,10 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
         for (int t = 0; t < BATCH; ++t)
           load_win<D, N32>(wv[t], wl[t], lane, e0, e1, pass, ac.P, ac.bid, ac.ent_q,
                                 ac.ent_unit, ac.ent_size, ac.ent_lead, ac.ent_slot, ac.s0);
+#pragma unroll
+        for (int t = 0; t < BATCH; ++t) landed_win(wv[t]);
+#pragma unroll
+        for (int t = 0; t < BATCH; ++t) finish_win(wv[t], pass);
         KP_PP_MARK(2);
 #pragma unroll
         for (int t = 0; t < BATCH; ++t) {
@@ -1135,23 +1225,39 @@ template <int D, bool N32, int B>
 __global__ __launch_bounds__(64 * KP_ACC_WPB) void k_accept(AccArgs ac, int32_t pass, int32_t use_list) {
   const int wv = blockIdx.x * KP_ACC_WPB + (threadIdx.x >> 6);
   const int nw = gridDim.x * KP_ACC_WPB;  // grid-stride: the grid may be smaller than the node count
-  const int32_t pf = ac.pass_flag[pass];
+  int32_t pf = ac.pass_flag[pass];
   if (ac.hflag && blockIdx.x == 0 && threadIdx.x == 0)  // final: plan `pass` has ended
     __hip_atomic_store(ac.hflag + pass, ac.htag | (pf ? 1 : 0), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
+  int4 r = make_int4(0, 0, 0, 0);
+  int32_t lim = ac.sp.N;
   if (use_list) {  // first record and count loaded together (nrec has 4 spare entries)
-    const int4 r = ac.nrec[wv];
-    const int32_t cnt = *ac.nl_count;
-    if (wv >= cnt || !pf) return;
-    accept_node<D, N32, B>(ac, pass, r.x, r.y, r.z);
-    for (int i = wv + nw; i < cnt; i += nw) {
-      const int4 ri = ac.nrec[i];
-      accept_node<D, N32, B>(ac, pass, ri.x, ri.y, ri.z);
+    r = ac.nrec[wv];
+    lim = *ac.nl_count;
+    landed(r.x);
+    landed(r.y);
+    landed(r.z);
+    landed(lim);
+  }
+  landed(pf);
+  if (wv >= lim || !pf) return;
+  // one call site (inlined copies of accept_node were tail-merged, and the
+  // merged blocks waited for every outstanding load); the node record is the
+  // wave's own, scalar, so the node's one- / multi-window branch is a scalar
+  // branch (as a lane-masked if/else it waited for the other side's loads)
+  for (int i = wv; i < lim; i += nw) {
+    int32_t nd = i, a0, a1;
+    if (use_list) {
+      if (i != wv) r = ac.nrec[i];
+      nd = r.x;
+      a0 = r.y;
+      a1 = r.z;
+    } else {
+      a0 = ac.seg_start[i];
+      a1 = ac.seg_end[i];
     }
-  } else {
-    if (!pf) return;
-    for (int node = wv; node < ac.sp.N; node += nw)
-      accept_node<D, N32, B>(ac, pass, node, ac.seg_start[node], ac.seg_end[node]);
+    accept_node<D, N32, B>(ac, pass, __builtin_amdgcn_readfirstlane(nd), __builtin_amdgcn_readfirstlane(a0),
+                           __builtin_amdgcn_readfirstlane(a1));
   }
 }
 

@@ -208,15 +208,20 @@ void k_score_topk(
   constexpr int SALT = PRE ? 0 : D + 2;
   __shared__ uint32_t sq[kFzMaxRows][PRE ? 1 : SQW];
   __shared__ __attribute__((aligned(16))) uint64_t sbuf[NW][kFzSurv];
-  __shared__ uint32_t spos[NG + NG / 64];   // per group (padded like the tile rows)
-  __shared__ uint32_t spos0[NG + NG / 64];  // tie mode 0: the select-phase tie bits
+  // per group (padded like the tile rows): [0] pos·mul, [1] tie mode 0's
+  // select-phase tie bits (one LDS object: a pointer chosen between two
+  // objects made the compiler wait for the record DMA before reading it)
+  __shared__ uint32_t sposb[2][NG + NG / 64];
+  uint32_t *const spos = sposb[0];
   __shared__ uint8_t scand[NW][64 * GPL];  // per wave: the (lane, group) pairs whose best reached T
   constexpr int RW = (2 * D + 4 + 3) & ~3;  // row record words, whole 16-B reads
-  // PRE: two buffers, the next chunk's records copied by the memory unit
-  // straight into LDS while the current chunk is scored (through VGPRs they
-  // spilled at the 80-VGPR budget)
-  constexpr int NRB = PRE ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) uint32_t srec[NRB][NW][kFzRC][RW];
+  // PRE: the next chunk's records are copied by the memory unit straight
+  // into the wave's LDS records (through VGPRs they spilled at the 80-VGPR
+  // budget) once the chunk's scores are in, so the copy is in flight during
+  // the select phase. (Issued at the chunk start into a second buffer, the
+  // copy was waited for at the chunk's first record read: the compiler's
+  // LDS-DMA wait covers every buffer of one LDS array.)
+  __shared__ __attribute__((aligned(16))) uint32_t srec[1][NW][kFzRC][RW];
   __shared__ int32_t su[PRE ? kFzMaxRows : 1];  // PRE: the rows' units
   auto pgi = [](int g) { return g + (g >> 6); };  // padded group index
   if (rows_dev) fit_rows(*rows_dev, min_rpb, rows, rows_per_block);
@@ -308,7 +313,7 @@ void k_score_topk(
     const int c = tile0 + 4 * tid;
     const uint32_t pos = (uint32_t)(c - wshift[c >> 7]);
     spos[pgi(tid)] = pos * mul;
-    spos0[pgi(tid)] = pos << (32 - TB);
+    sposb[1][pgi(tid)] = pos << (32 - TB);
   }
   KP_FZ_PROF_MARK(0);
   __syncthreads();  // requests and positions staged
@@ -319,28 +324,30 @@ void k_score_topk(
   for (int d = 0; d < D; ++d) wv[d] = in_vgpr(sp.w[d]);
   const int32_t waffv = in_vgpr(sp.w_affinity);
   const int rsh = 32 - tbits;  // select-phase tie bits: tbits <= ksh (= ksh but in tests)
-  // PRE: this wave's class and its row records (kp_score.hip k_unit_rec), RW/4
-  // 16-B pieces per row, one per lane, the next chunk's loaded while the
-  // current one is scored
+  // PRE: this wave's class (wave-uniform: scalar) and its row records
+  // (kp_score.hip k_unit_rec), RW/4 16-B pieces per row, one per lane, the
+  // next chunk's loaded during the current chunk's select
   constexpr int Q4 = RW / 4;
   static_assert(!PRE || kFzRC * Q4 <= 64, "one record piece per lane");
-  const int cls = PRE ? tcls[(tile0 >> 7) + wave] : 0;
-  const uint4 *crec4 = reinterpret_cast<const uint4 *>(crec);
-  // rows c .. c + kFzRC - 1 into srec[b][wave]: lane l copies 16-B piece l % Q4
-  // of row l / Q4 to byte 16·l of the buffer (the LDS DMA's lane layout)
-  auto rec_dma = [&](int c, int b) {
-    if (lane < min(kFzRC, nr - c) * Q4)
-      __builtin_amdgcn_global_load_lds(crec4 + ((int64_t)su[c + lane / Q4] * nfc + cls) * Q4 + lane % Q4,
-                                       (void __attribute__((address_space(3))) *)&srec[b][wave][0][0], 16, 0, 0);
+  const int cls = PRE ? tcls[(tile0 >> 7) + __builtin_amdgcn_readfirstlane(wave)] : 0;
+  const uint4 *crec4 = reinterpret_cast<const uint4 *>(crec) + cls * Q4;
+  // rows c .. c + kFzRC - 1 into srec[0][wave]: lane l copies 16-B piece l % Q4
+  // of row l / Q4 to byte 16·l of the buffer (the LDS DMA's lane layout). The
+  // lane terms are recomputed per call (hoisted out of the chunk loop they
+  // were spilled)
+  auto rec_dma = [&](int c) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    if (ln < min(kFzRC, nr - c) * Q4)
+      __builtin_amdgcn_global_load_lds(crec4 + (int64_t)su[c + ln / Q4] * (nfc * Q4) + ln % Q4,
+                                       (void __attribute__((address_space(3))) *)&srec[0][wave][0][0], 16, 0, 0);
   };
-  if (PRE) rec_dma(0, 0);
+  if (PRE) rec_dma(0);
   for (int c0 = 0; c0 < nr; c0 += kFzRC) {
     const int cr = min(kFzRC, nr - c0);
     const int buf = NB == 2 ? (c0 / kFzRC) & 1 : 0;
-    const int rb = NRB == 2 ? (c0 / kFzRC) & 1 : 0;
     if constexpr (PRE) {  // 1a. the chunk's row records: one 16-B piece per lane
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this chunk's copy has landed
-      if (c0 + kFzRC < nr) rec_dma(c0 + kFzRC, rb ^ 1);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -420,7 +427,7 @@ void k_score_topk(
 #endif
       for (int i = 0; i < cr; ++i) {
         RowRec<RW> cur;
-        cur.load(srec[rb][wave][i]);
+        cur.load(srec[0][wave][i]);
         const uint32_t wq = cur[2 * D + 2], qg = cur[D], af = cur[D + 1];
         const int32_t wfr = (int32_t)cur[2 * D + 3];
         // the row's terms, wave-uniform: a request no column of the wave's
@@ -478,6 +485,10 @@ void k_score_topk(
     }
     KP_FZ_PROF_MARK(3);
     __syncthreads();  // the chunk's scores are in LDS
+    // the next chunk's records (the wave's own LDS records, read by the score
+    // loop above): in flight during the select phase, which reads other LDS
+    if constexpr (PRE)
+      if (c0 + kFzRC < nr) rec_dma(c0 + kFzRC);
     KP_FZ_PROF_MARK(4);
     // 2. top-K of this tile for row `wave` of the chunk. LDS holds s + 1
     //    (0 = infeasible); a column's 32-bit key is (s + 1) << ksh | the top
@@ -496,7 +507,7 @@ void k_score_topk(
       const int64_t row = r0 + c0 + i;
       const uint32_t nsl = ~sq[c0 + i][SALT];
       // select-phase tie bits: (nst - tsp[g] - j * mt) >> rsh
-      const uint32_t *tsp = tie0 ? spos0 : spos;
+      const uint32_t *tsp = sposb[tie0 ? 1 : 0];
       const uint32_t nst = tie0 ? (spos[0] + (uint32_t)(kFzTile - 1)) << (32 - TB) : nsl,
                      mt = tie0 ? 1u << (32 - TB) : mul;
       // lane L's 16 columns are the 4-column groups L + 64k, k < GPL
