@@ -376,14 +376,30 @@ __global__ void k_csr_place(int32_t A, int32_t K, int32_t D, int32_t U, int64_t 
                             int32_t *__restrict__ ent_size, int32_t *__restrict__ ent_lead,
                             int64_t *__restrict__ ent_q) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int32_t Aa = A_dev ? min(A, *A_dev) : A;
-  if (t >= (int64_t)Aa * K) return;
-  const int32_t n = cand[t];
+  if (t >= (int64_t)A * K) return;  // the host bound: cand / act are readable below it
+  // two memory levels: {device slot count, candidate, unit}, then {the
+  // node's segment and bitmap word, the unit's size / leader / request}
+  int32_t adev = A_dev ? *A_dev : A;
+  int32_t n = cand[t];
   const int32_t a = (int32_t)(t / K);
-  const int32_t u = act[a];
-  if (n < 0) return;
-  const int32_t ss = seg_start[n], len = cnt[n];
-  const uint2 ri = rowinfo[(int64_t)n * Wb + (a >> 5)];
+  int32_t u = act[a];
+  landed(adev);
+  landed(n);
+  landed(u);
+  if (t >= (int64_t)min(A, adev) * K || n < 0) return;
+  int32_t ss = seg_start[n], len = cnt[n];
+  uint2 ri = rowinfo[(int64_t)n * Wb + (a >> 5)];
+  int32_t usz = size[u], uld = leader[u];
+  int64_t qv[KP_MAX_DIMS];
+#pragma unroll
+  for (int d = 0; d < KP_MAX_DIMS; ++d) qv[d] = d < D ? q[(int64_t)d * U + u] : 0;
+  landed(ss);
+  landed(len);
+  landed(ri.x);
+  landed(usz);
+  landed(uld);
+#pragma unroll
+  for (int d = 0; d < KP_MAX_DIMS; ++d) landed(qv[d]);
   const int32_t e = ss + (int32_t)ri.x + __popc(ri.y & ((1u << (a & 31)) - 1u));
   // bit 31: the entry's bidder row spans >= bmin_windows windows (the plan
   // keeps exact per-pass window minima for those rows only)
@@ -392,9 +408,11 @@ __global__ void k_csr_place(int32_t A, int32_t K, int32_t D, int32_t U, int64_t 
   // operands of entry e in bidder order (k_accept's window loads)
   ent_unit[e] = u;
   ent_slot[e] = a;
-  ent_size[e] = size[u];
-  ent_lead[e] = leader[u];
-  for (int d = 0; d < D; ++d) ent_q[(int64_t)d * P + e] = q[(int64_t)d * U + u];
+  ent_size[e] = usz;
+  ent_lead[e] = uld;
+#pragma unroll
+  for (int d = 0; d < KP_MAX_DIMS; ++d)
+    if (d < D) ent_q[(int64_t)d * P + e] = qv[d];
 }
 
 // The same placement in two phases per 1,024-thread workgroup of S = 1024 / K
@@ -439,12 +457,24 @@ __global__ __launch_bounds__(1024) void k_csr_place_t(
     const int64_t a = a0 + al;
     const int32_t e = se[al * (K + 1) + j];
     if (a < Aa && e >= 0) {
-      const int32_t u = act[a];
+      int32_t u = act[a];
+      landed(u);
+      // the unit's operands in one memory level
+      int32_t usz = size[u], uld = leader[u];
+      int64_t qv[KP_MAX_DIMS];
+#pragma unroll
+      for (int d = 0; d < KP_MAX_DIMS; ++d) qv[d] = d < D ? q[(int64_t)d * U + u] : 0;
+      landed(usz);
+      landed(uld);
+#pragma unroll
+      for (int d = 0; d < KP_MAX_DIMS; ++d) landed(qv[d]);
       ent_unit[e] = u;
       ent_slot[e] = (int32_t)a;
-      ent_size[e] = size[u];
-      ent_lead[e] = leader[u];
-      for (int d = 0; d < D; ++d) ent_q[(int64_t)d * P + e] = q[(int64_t)d * U + u];
+      ent_size[e] = usz;
+      ent_lead[e] = uld;
+#pragma unroll
+      for (int d = 0; d < KP_MAX_DIMS; ++d)
+        if (d < D) ent_q[(int64_t)d * P + e] = qv[d];
     }
   }
 }
@@ -1136,7 +1166,6 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
     decide_window<D, N32>(wv, rem, add, lane, node, o);
     KP_PP_MARK(3);
   } else {
-    node_load();
     constexpr int BATCH = B;  // flagged windows whose operands are loaded together
     for (int wb = w0; wb <= w1; wb += 64) {
       const int wi = wb + lane;
@@ -1154,7 +1183,8 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
         braw[d] = mine && lrow ? (uint64_t)ac.bmin[(int64_t)d * ac.nwin + wi] : 0;
       }
       wf = mine ? ac.win[wi] : -1;
-      if (wb == w0) {  // the first chunk's flags were loaded with the node's operands
+      if (wb == w0) {  // the first chunk's flags land with the node's operands
+        node_load();   // (issued here: the loop head waits for everything outstanding)
         node_landed();
         landed(wf);
 #pragma unroll

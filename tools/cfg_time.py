@@ -19,7 +19,7 @@ with Placer(device=0) as pl:
     pl.load_nodes(w.cap, w.used, w.topo)
     pl.load_jobs(w.req, w.prio, w.gang_id, w.gang_size)
     ts = []
-    for it in range(6):
+    for it in range(int(os.environ.get("SOLVES", "6"))):
         pl.reset_nodes()
         t = time.perf_counter()
         st = pl.solve(p)
