@@ -743,20 +743,29 @@ __global__ __launch_bounds__(64 * KP_MERGE_WPB) void k_merge_tour(ScoreParams sp
     return;
   }
   const int row = blockIdx.x * kMergeWPB + wave;
-  const bool live = row < rows && !(rows_dev && row >= *rows_dev);  // wave-uniform
   const int K = sp.n_cand, M = ntiles * K;
   int32_t unit = 0, mine = -1;
-  if (live) {
+  uint32_t sl = 0u;  // the unit's tie salt (rotated ties)
+  bool live = false;
+  if (row < rows) {  // wave-uniform
+    // the device row count and the row's unit are loaded with the first keys
+    // (then the unit's tie salt while the keys go to LDS): no dependent
+    // memory level before the staging
+    int32_t rdev = rows_dev ? *rows_dev : rows;
+    int32_t u0 = rows_unit[row];
     uint64_t *L = slist + (int64_t)wave * M;
-    const uint64_t *src = part + (int64_t)row * M;
+    const uint64_t *src = part + (int64_t)row * M;  // readable for every row < rows
     // the row's lists staged in batches of 8 loads per lane issued together (a
     // load-then-store loop waited one memory latency per 64 keys)
     for (int b0 = 0; b0 < M; b0 += 64 * kMergeLoadBatch) {
       uint64_t x[kMergeLoadBatch];
 #pragma unroll
-      for (int u = 0; u < kMergeLoadBatch; ++u) {
-        const int e = b0 + 64 * u + lane;
-        x[u] = e < M ? src[e] : 0ull;
+      for (int u = 0; u < kMergeLoadBatch; ++u)  // unmasked (clamped): exact wait counts below
+        x[u] = src[min(b0 + 64 * u + lane, M - 1)];
+      if (b0 == 0) {
+        landed(rdev);  // issued before the keys: the keys stay in flight
+        landed(u0);
+        if (sp.tie_rotated && row < rdev) sl = salt[u0];  // a live row's unit only
       }
 #pragma unroll
       for (int u = 0; u < kMergeLoadBatch; ++u) {
@@ -764,11 +773,14 @@ __global__ __launch_bounds__(64 * KP_MERGE_WPB) void k_merge_tour(ScoreParams sp
         if (e < M) L[e] = x[u];
       }
     }
+    live = row < rdev;
+    unit = u0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    unit = rows_unit[row];
-    const uint32_t sl = sp.tie_rotated ? salt[unit] : 0u;
+  }
+  if (live) {
+    const uint64_t *L = slist + (int64_t)wave * M;
     const uint32_t inv = sp.tie_rotated ? kTieMulInv : 1u;
     const int32_t mypos = merge_tour_row<LPL>(L, ntiles, K, sl, inv, lane);
     // canonical position -> node (a position is always < N)

@@ -26,6 +26,7 @@ for cfg in c3 c4; do
   [ "$cfg" = c4 ] && [ "$SKIP_C4" = 1 ] && continue
   python3 tools/kstats_cmp.py $(for l in $LIBS; do echo $OUT/$l.$cfg/run_kernel_stats.csv; done)
   [ "$cfg" = c3 ] && for rep in $(seq 2 ${REPS:-1}); do
-    python3 tools/kstats_cmp.py $(for l in $LIBS; do echo $OUT/$l.$cfg.r$rep/run_kernel_stats.csv; done) | head -5
+    python3 tools/kstats_cmp.py $(for l in $LIBS; do echo $OUT/$l.$cfg.r$rep/run_kernel_stats.csv; done) 2>/dev/null | head -5 || true
   done
 done
+true

@@ -17,5 +17,5 @@ for v in $VALS; do
 done
 for cfg in c3 c4; do
   [ "$cfg" = c4 ] && [ "$SKIP_C4" = 1 ] && continue
-  python3 tools/kstats_cmp.py $(for v in $VALS; do echo $OUT/$v.$cfg/run_kernel_stats.csv; done) | head -6
+  python3 tools/kstats_cmp.py $(for v in $VALS; do echo $OUT/$v.$cfg/run_kernel_stats.csv; done) 2>/dev/null | head -6 || true
 done
