@@ -343,6 +343,7 @@ int create_one(kp_ctx **out, int device, int world, int rank, const void *nccl_i
   if (const char *e = knob("KP_ACC_LIST")) c->acc_list = std::atoi(e);
   if (const char *e = knob("KP_ACC_BIG_RATIO")) c->acc_big_ratio = std::max(0, std::atoi(e));
   if (const char *e = knob("KP_BMIN_WIN")) c->bmin_windows = std::max(1, std::atoi(e));
+  if (const char *e = knob("KP_BMIN_DIMS")) c->bmin_dims = (int32_t)std::strtol(e, nullptr, 0);
   if (const char *e = knob("KP_PASS_FOLLOW")) c->pass_follow = std::max(0, std::min(64, std::atoi(e)));
   if (const char *e = knob("KP_KEYS_MERGE")) c->keys_merge_enabled = std::atoi(e) != 0;
   if (const char *e = knob("KP_ROUND_BEGIN")) c->round_begin = std::atoi(e) != 0;
@@ -591,6 +592,18 @@ static int load_nodes_impl(kp_ctx *c, int32_t N, int32_t D, const int64_t *cap,
   c->D = D;
   c->max_cap = 0;
   for (int64_t i = 0; i < (int64_t)D * N; ++i) c->max_cap = std::max(c->max_cap, cap[i]);
+  // per-dim totals for the automatic bid-minima dims (a heuristic: every
+  // 4th node, so the load stays one pass over the table)
+  for (int d = 0; d < KP_MAX_DIMS; ++d) {
+    double cs = 0, us = 0;
+    if (d < D)
+      for (int32_t n = 0; n < N; n += 4) {
+        cs += (double)cap[(int64_t)d * N + n];
+        us += used ? (double)used[(int64_t)d * N + n] : 0.0;
+      }
+    c->cap_sum[d] = cs;
+    c->used_sum[d] = us;
+  }
   c->caps32 = c->max_cap < ((int64_t)1 << 32);
   // the fused layout pays off while the padding stays small (few capacity
   // classes); the merge holds at most 2,048 keys per row (tiles x K)
@@ -746,6 +759,14 @@ static int load_jobs_impl(kp_ctx *c, int32_t J, const int64_t *req, const int32_
   c->u_hi = (int32_t)((int64_t)U * (c->rank + 1) / c->world);
   c->max_req = 0;
   for (int64_t i = 0; i < (int64_t)D * J; ++i) c->max_req = std::max(c->max_req, req[i]);
+  // pending requests per dim, on the node totals' scale: every 16th job x 16
+  // against every 4th node x 4 (the automatic bid-minima dims only)
+  for (int d = 0; d < KP_MAX_DIMS; ++d) {
+    double rs = 0;
+    if (d < D)
+      for (int32_t j = 0; j < J; j += 16) rs += (double)req[(int64_t)d * J + j];
+    c->req_sum[d] = rs * 16.0 / 4.0;
+  }
   c->reqs32 = c->max_req < ((int64_t)1 << 32);
   c->fits32 = c->caps32 && c->reqs32;
   c->jobs_loaded = true;

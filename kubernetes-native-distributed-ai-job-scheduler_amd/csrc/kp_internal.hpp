@@ -306,6 +306,12 @@ struct kp_ctx {
   // per-pass window bid minima (plan atomics) on top of the round's request
   // minima; shorter rows only flags
   int32_t bmin_windows = 64;
+  // dims with per-pass bid minima (bit d; bit 0 always: it carries the pass
+  // tag); 0 = automatic (kp_pass.hip bmin_dims_of), KP_BMIN_DIMS overrides
+  int32_t bmin_dims = 0;
+  // per-dim totals of the loaded tables (capacity, usage at load, pending
+  // requests): the automatic choice of bid-minima dims
+  double cap_sum[KP_MAX_DIMS] = {0}, used_sum[KP_MAX_DIMS] = {0}, req_sum[KP_MAX_DIMS] = {0};
   int32_t acc_big_ratio = 48;  // k_accept's long-row form when A*K >= ratio * N (0: never)
   bool hpass_on = false;
   void *stage = nullptr;  // pinned staging of kp_load_jobs' unit arrays

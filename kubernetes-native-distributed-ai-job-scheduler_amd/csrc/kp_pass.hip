@@ -537,6 +537,7 @@ struct PlanArgs {
   const int64_t *ent_q;
   int64_t *winmin;
   int64_t *bmin;  // long rows: per-window bid minima of the pass
+  int32_t bmin_dims;  // dims with bid minima (bit d; bit 0 always)
   uint32_t key_off;        // W32 member loop: 64 * w_spread + 1 (plan_key_ok)
   uint64_t *pp;            // KP_PASS_PROFILE only
   const SolveStats *st;    // KP_PASS_PROFILE only (round index)
@@ -820,6 +821,7 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
       pend &= ~grp;
 #pragma unroll
       for (int d = 0; d < D; ++d) {
+        if (!((pa.bmin_dims >> d) & 1)) continue;  // untracked dim (dim 0 always: the tag)
         const uint64_t need = (uint64_t)planned * (uint64_t)qq[d];
         const uint32_t nlo = (uint32_t)need, nhi = (uint32_t)(need >> 32);
         uint64_t mn = ~0ull;
@@ -1099,6 +1101,7 @@ struct AccArgs {
   const int64_t *bmin;    // long rows: this pass's smallest bid per window, tagged (k_plan)
   int64_t nwin;
   int32_t bmin_windows;   // rows spanning at least this many windows are long
+  int32_t bmin_dims;      // dims with bid minima (bit d; bit 0 always)
   AcceptOut o;
   // host-followed passes: this pass's flag, tagged with the round serial, to
   // coherent host memory (the host enqueues further passes only while it is set)
@@ -1180,7 +1183,7 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         wmin[d] = mine ? ac.winmin[(int64_t)d * ac.nwin + wi] : 0;
-        braw[d] = mine && lrow ? (uint64_t)ac.bmin[(int64_t)d * ac.nwin + wi] : 0;
+        braw[d] = mine && lrow && ((ac.bmin_dims >> d) & 1) ? (uint64_t)ac.bmin[(int64_t)d * ac.nwin + wi] : 0;
       }
       wf = mine ? ac.win[wi] : -1;
       if (wb == w0) {  // the first chunk's flags land with the node's operands
@@ -1297,6 +1300,28 @@ static bool plan_key_ok(const ScoreParams &sp, int lb) {
   return bound < ((int64_t)1 << (32 - lb));
 }
 
+// Dims whose per-pass bid minima the plan keeps for long bidder rows: dim 0
+// (its entry carries the pass tag) and the most contended other dim, by
+// (usage + pending requests) / capacity over the loaded tables. Each tracked
+// dim costs one device-scope atomic per long-row bid and window; on config #4
+// dims {0, 2} prune as well as all four (k_accept 58 vs 60 ms per 3 solves)
+// with half the atomics (k_plan 163 vs 193 ms), DESIGN.md A.4. Pruning never
+// changes a result, only which windows accept reads.
+static int32_t bmin_dims_of(const kp_ctx *c) {
+  if (c->bmin_dims) return c->bmin_dims | 1;
+  int best = 0;
+  double bp = -1.0;
+  for (int d = 1; d < c->D && d < KP_MAX_DIMS; ++d)
+    if (c->cap_sum[d] > 0) {
+      const double p = (c->used_sum[d] + c->req_sum[d]) / c->cap_sum[d];
+      if (p > bp) {
+        bp = p;
+        best = d;
+      }
+    }
+  return 1 | (best > 0 ? 1 << best : 0);
+}
+
 static PlanArgs plan_args(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass,
                           const int32_t *A_dev) {
   PlanArgs pa;
@@ -1335,6 +1360,7 @@ static PlanArgs plan_args(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t p
   pa.ent_q = c->d.ent_q;
   pa.winmin = c->d.winmin;
   pa.bmin = c->d.bmin;
+  pa.bmin_dims = bmin_dims_of(c);
   pa.node_list = c->d.node_list;
   pa.nl_count = c->d.counters + 32;
   pa.seg_start = c->d.seg_start;
@@ -1369,6 +1395,7 @@ static AccArgs acc_args(kp_ctx *c, const ScoreParams &sp, int64_t P) {
   ac.winmin = c->d.winmin;
   ac.bmin = c->d.bmin;
   ac.bmin_windows = c->bmin_windows;
+  ac.bmin_dims = bmin_dims_of(c);
   ac.nwin = (P + 63) / 64 + 64;
   AcceptOut &o = ac.o;
   o.N = c->N;
