@@ -306,8 +306,8 @@ struct kp_ctx {
   // per-pass window bid minima (plan atomics) on top of the round's request
   // minima; shorter rows only flags
   int32_t bmin_windows = 64;
-  // dims with per-pass bid minima (bit d; bit 0 always: it carries the pass
-  // tag); 0 = automatic (kp_pass.hip bmin_dims_of), KP_BMIN_DIMS overrides
+  // dims with per-pass bid minima (bit d); 0 = automatic (kp_pass.hip
+  // bmin_dims_of: the two most contended), KP_BMIN_DIMS overrides
   int32_t bmin_dims = 0;
   // per-dim totals of the loaded tables (capacity, usage at load, pending
   // requests): the automatic choice of bid-minima dims

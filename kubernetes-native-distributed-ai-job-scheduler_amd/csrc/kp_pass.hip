@@ -537,7 +537,7 @@ struct PlanArgs {
   const int64_t *ent_q;
   int64_t *winmin;
   int64_t *bmin;  // long rows: per-window bid minima of the pass
-  int32_t bmin_dims;  // dims with bid minima (bit d; bit 0 always)
+  int32_t bmin_dims;  // dims with bid minima (bit d)
   uint32_t key_off;        // W32 member loop: 64 * w_spread + 1 (plan_key_ok)
   uint64_t *pp;            // KP_PASS_PROFILE only
   const SolveStats *st;    // KP_PASS_PROFILE only (round index)
@@ -821,7 +821,7 @@ __device__ __forceinline__ void plan_wave(const PlanArgs &pa, int32_t pass, int 
       pend &= ~grp;
 #pragma unroll
       for (int d = 0; d < D; ++d) {
-        if (!((pa.bmin_dims >> d) & 1)) continue;  // untracked dim (dim 0 always: the tag)
+        if (!((pa.bmin_dims >> d) & 1)) continue;  // untracked dim
         const uint64_t need = (uint64_t)planned * (uint64_t)qq[d];
         const uint32_t nlo = (uint32_t)need, nhi = (uint32_t)(need >> 32);
         uint64_t mn = ~0ull;
@@ -1101,7 +1101,7 @@ struct AccArgs {
   const int64_t *bmin;    // long rows: this pass's smallest bid per window, tagged (k_plan)
   int64_t nwin;
   int32_t bmin_windows;   // rows spanning at least this many windows are long
-  int32_t bmin_dims;      // dims with bid minima (bit d; bit 0 always)
+  int32_t bmin_dims;      // dims with bid minima (bit d)
   AcceptOut o;
   // host-followed passes: this pass's flag, tagged with the round serial, to
   // coherent host memory (the host enqueues further passes only while it is set)
@@ -1199,7 +1199,11 @@ __device__ __forceinline__ void accept_node(const AccArgs &ac, int32_t pass, int
         if (nf != pass) return;
         KP_PP_WORK();
       }
-      uint64_t flagged = __ballot(wf == pass || (braw[0] >> 48) == (uint64_t)(pass + 1));
+      // a long-row bid of this pass tags every tracked dim's entry
+      bool ltag = false;
+#pragma unroll
+      for (int d = 0; d < D; ++d) ltag |= (braw[d] >> 48) == (uint64_t)(pass + 1);
+      uint64_t flagged = __ballot(wf == pass || ltag);
       // the bid minima bound every bid of the window unless a short row bid
       // in it too (a dim without this pass's tag: no long-row bid)
       if (lrow) {
@@ -1300,26 +1304,32 @@ static bool plan_key_ok(const ScoreParams &sp, int lb) {
   return bound < ((int64_t)1 << (32 - lb));
 }
 
-// Dims whose per-pass bid minima the plan keeps for long bidder rows: dim 0
-// (its entry carries the pass tag) and the most contended other dim, by
-// (usage + pending requests) / capacity over the loaded tables. Each tracked
-// dim costs one device-scope atomic per long-row bid and window; on config #4
-// dims {0, 2} prune as well as all four (k_accept 58 vs 60 ms per 3 solves)
-// with half the atomics (k_plan 163 vs 193 ms), DESIGN.md A.4. Pruning never
+// Dims whose per-pass bid minima the plan keeps for long bidder rows: the two
+// most contended, by (usage + pending requests) / capacity over the loaded
+// tables (every tracked dim's entry carries the pass tag). Each tracked dim
+// costs one device-scope atomic per long-row bid and window; on config #4 the
+// two (cpu, GPU count) prune as well as all four (k_accept 58 vs 60 ms per 3
+// solves) with half the atomics (k_plan 163 vs 193 ms), while either alone
+// prunes far less (k_accept 122 / 310 ms), DESIGN.md A.4. Pruning never
 // changes a result, only which windows accept reads.
 static int32_t bmin_dims_of(const kp_ctx *c) {
-  if (c->bmin_dims) return c->bmin_dims | 1;
-  int best = 0;
-  double bp = -1.0;
-  for (int d = 1; d < c->D && d < KP_MAX_DIMS; ++d)
-    if (c->cap_sum[d] > 0) {
-      const double p = (c->used_sum[d] + c->req_sum[d]) / c->cap_sum[d];
-      if (p > bp) {
-        bp = p;
-        best = d;
-      }
+  const int D = std::min(c->D, KP_MAX_DIMS);
+  if (c->bmin_dims) {  // forced: at least one dim < D
+    const int32_t m = c->bmin_dims & ((1 << D) - 1);
+    return m ? m : 1;
+  }
+  int b0 = -1, b1 = -1;
+  double p0 = -1.0, p1 = -1.0;
+  for (int d = 0; d < D; ++d) {
+    const double p = c->cap_sum[d] > 0 ? (c->used_sum[d] + c->req_sum[d]) / c->cap_sum[d] : 0.0;
+    if (p > p0) {
+      b1 = b0, p1 = p0;
+      b0 = d, p0 = p;
+    } else if (p > p1) {
+      b1 = d, p1 = p;
     }
-  return 1 | (best > 0 ? 1 << best : 0);
+  }
+  return (b0 >= 0 ? 1 << b0 : 1) | (b1 >= 0 ? 1 << b1 : 0);
 }
 
 static PlanArgs plan_args(kp_ctx *c, const ScoreParams &sp, int32_t A, int32_t pass,
